@@ -1,0 +1,448 @@
+// renderer.cpp — the rt_* C-ABI: device buffers, frame protocol and kernel launches on one HIP stream.
+//
+// Replaces the reference's wgpu Renderer (hucancode/hello-raytracing src/renderer.rs): the group0/group1
+// bind-group buffers become device allocations owned by the handle, queue.write_buffer becomes a
+// copy + layout conversion (AoS reference PODs -> the kernel's layout), and draw() becomes a kernel
+// launch. There is no CPU fallback: without a gfx950 device every call that needs one returns
+// RT_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hrt.h"
+#include "host/scene.hpp"
+#include "rt_device.hpp"
+
+hipError_t hrt_launch_render(int mode, const hrt_dev::KParams& P, hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RT_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* ptr = nullptr;
+    size_t cap = 0;  // elements
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+};
+
+template <typename T>
+int ensure(DevBuf<T>& b, size_t n) {
+    if (n <= b.cap && b.ptr) return RT_OK;
+    b.release();
+    size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void**)&b.ptr, bytes);
+    if (e != hipSuccess) return fail(RT_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    b.cap = std::max<size_t>(n, 1);
+    return RT_OK;
+}
+
+int check_device(int* dev_out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(RT_ERR_DEVICE, "no HIP device visible (the renderer has no CPU fallback)");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RT_ERR_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
+    *dev_out = dev;
+    return RT_OK;
+}
+
+uint32_t local_rows_of(uint32_t H, uint32_t row0, uint32_t step) {
+    if (row0 >= H || step == 0) return 0;
+    return (H - row0 + step - 1) / step;
+}
+
+}  // namespace
+
+struct rt_renderer {
+    int device = 0;
+    int mode = RT_MODE_SPHERE;
+    uint32_t width = 0, height = 0;
+    rt_params params{};
+    hrt::Camera camera{};
+    bool has_camera = false;
+    uint32_t time = 0, frame_count = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+
+    DevBuf<float> image;
+    DevBuf<float4> sph_geo;
+    DevBuf<hrt_dev::SphereAux> sph_aux;
+    uint32_t n_spheres = 0;
+    DevBuf<float4> nodes;
+    DevBuf<hrt_dev::TriDev> tris;
+    DevBuf<hrt_dev::MatDev> mats;
+    uint32_t bvh_n = 0, bvh_m = 0;
+    DevBuf<unsigned long long> counter;
+
+    // host copy of the spheres (slot arrays are rebuilt when min_sphere_slots changes)
+    std::vector<hrt::Sphere> spheres;
+
+    rt_stats stats{};
+    bool timing_pending = false;
+
+    uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
+    size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
+};
+
+namespace {
+
+int zero_image(rt_renderer* r) {
+    int rc = ensure(r->image, r->image_floats());
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(r->image.ptr, 0, std::max<size_t>(r->image_floats(), 1) * sizeof(float), r->stream));
+    return RT_OK;
+}
+
+int upload_spheres(rt_renderer* r) {
+    const uint32_t nslots = std::max<uint32_t>((uint32_t)r->spheres.size(), r->params.min_sphere_slots);
+    std::vector<float4> geo(nslots, float4{0.0f, 0.0f, 0.0f, 0.0f});
+    std::vector<hrt_dev::SphereAux> aux(nslots);
+    std::memset(aux.data(), 0, aux.size() * sizeof(aux[0]));
+    for (size_t i = 0; i < r->spheres.size(); i++) {
+        const hrt::Sphere& s = r->spheres[i];
+        const float rr = s.radius * s.radius;  // radius*radius, shader_sphere.wgsl:142
+        geo[i] = float4{s.center.x, s.center.y, s.center.z, rr};
+        aux[i] = hrt_dev::SphereAux{s.center.x, s.center.y, s.center.z, s.radius,
+                                    s.material.albedo.x, s.material.albedo.y, s.material.albedo.z,
+                                    s.material.params.x, s.material.kind, 0, 0, 0};
+    }
+    int rc = ensure(r->sph_geo, nslots);
+    if (!rc) rc = ensure(r->sph_aux, nslots);
+    if (rc) return rc;
+    if (nslots) {
+        HIP_TRY(hipMemcpyAsync(r->sph_geo.ptr, geo.data(), nslots * sizeof(float4), hipMemcpyHostToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->sph_aux.ptr, aux.data(), nslots * sizeof(aux[0]), hipMemcpyHostToDevice, r->stream));
+        HIP_TRY(hipStreamSynchronize(r->stream));  // host staging vectors die here
+    }
+    r->n_spheres = nslots;
+    return RT_OK;
+}
+
+int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime) {
+    if (!r->has_camera) return fail(RT_ERR_STATE, "rt_set_camera must be called before drawing");
+    if (r->mode == RT_MODE_SPHERE && r->sph_geo.ptr == nullptr) {
+        int rc = upload_spheres(r);  // empty scene: min_sphere_slots zero slots, like an unwritten buffer
+        if (rc) return rc;
+    }
+    int rc = ensure(r->counter, 1);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, sizeof(unsigned long long), r->stream));
+
+    hrt_dev::KParams P{};
+    const hrt::Camera& c = r->camera;
+    const float* cam = &c.eye.x;
+    for (int i = 0; i < 4; i++) {
+        P.eye[i] = cam[i];
+        P.dir[i] = cam[4 + i];
+        P.up[i] = cam[8 + i];
+        P.right[i] = cam[12 + i];
+    }
+    P.focal = c.params.x;
+    P.blur = c.params.y;
+    P.k = std::tan(c.params.z * 0.5f);  // tan(camera.fov*0.5), make_ray :124 (libm tanf, as the oracle)
+    P.aspect = (float)r->width / (float)r->height;
+    P.wm1 = (float)r->width - 1.0f;
+    P.hm1 = (float)r->height - 1.0f;
+    P.W = r->width;
+    P.H = r->height;
+    P.dtime = dtime;
+    P.bounces = r->params.bounces;
+    P.ema_cap = (float)r->params.ema_cap;
+    P.nslots = r->mode == RT_MODE_TRIS ? 0u : r->n_spheres;
+    P.n = r->mode == RT_MODE_SPHERE ? 0u : r->bvh_n;
+    P.m = r->mode == RT_MODE_SPHERE ? 0u : r->bvh_m;
+    P.row0 = r->params.row0;
+    P.row_step = r->params.row_step;
+    P.nrows = r->local_rows();
+    P.image = r->image.ptr;
+    P.sph_geo = r->sph_geo.ptr;
+    P.sph_aux = r->sph_aux.ptr;
+    P.nodes = r->nodes.ptr;
+    P.tris = r->tris.ptr;
+    P.mats = r->mats.ptr;
+    P.counter = r->counter.ptr;
+
+    const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
+    HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+    uint32_t launches = 0;
+    for (uint32_t done = 0; done < count; done += fpl) {
+        P.nframes = std::min(fpl, count - done);
+        P.time0 = time0 + done * dtime;
+        P.frame0 = r->frame_count + done;
+        HIP_TRY(hrt_launch_render(r->mode, P, r->stream));
+        launches++;
+    }
+    HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
+    r->frame_count += count;  // end_frame, renderer.rs:409
+    r->stats = rt_stats{};
+    r->stats.samples = (uint64_t)count * P.nrows * r->width;
+    r->stats.launches = launches;
+    r->stats.local_rows = P.nrows;
+    r->timing_pending = true;
+    return RT_OK;
+}
+
+int finish_stats(rt_renderer* r) {
+    if (!r->timing_pending) return RT_OK;
+    HIP_TRY(hipEventSynchronize(r->ev_stop));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
+    unsigned long long q = 0;
+    HIP_TRY(hipMemcpy(&q, r->counter.ptr, sizeof(q), hipMemcpyDeviceToHost));
+    r->stats.kernel_ms = ms;
+    r->stats.queries = q;
+    r->timing_pending = false;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* rt_build_info(void) { return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_render<sphere|tris|mixed>"; }
+
+int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
+    if (!out || width == 0 || height == 0) return fail(RT_ERR_ARG, "rt_create: null out or zero size");
+    if (mode < RT_MODE_SPHERE || mode > RT_MODE_MIXED) return fail(RT_ERR_ARG, "rt_create: bad mode");
+    *out = nullptr;
+    int dev = 0;
+    int rc = check_device(&dev);
+    if (rc) return rc;
+    rt_renderer* r = new rt_renderer();
+    r->device = dev;
+    r->mode = mode;
+    r->width = width;
+    r->height = height;
+    r->params.bounces = mode == RT_MODE_SPHERE ? 10u : 5u;  // BOUNCE_MAX
+    r->params.ema_cap = RT_SAMPLE_FRAME;
+    // arrayLength(&scene) = the 100-slot buffer in the sphere program; no such floor in the others.
+    r->params.min_sphere_slots = mode == RT_MODE_SPHERE ? RT_MAX_OBJECT_IN_SCENE : 0u;
+    r->params.row0 = 0;
+    r->params.row_step = 1;
+    r->params.frames_per_launch = 32;
+    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
+        rt_destroy(r);
+        return fail(RT_ERR_DEVICE, "rt_create: stream/event creation failed");
+    }
+    rc = zero_image(r);
+    if (rc) {
+        rt_destroy(r);
+        return rc;
+    }
+    *out = r;
+    return RT_OK;
+}
+
+int rt_destroy(rt_renderer* r) {
+    if (!r) return RT_OK;
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    r->image.release();
+    r->sph_geo.release();
+    r->sph_aux.release();
+    r->nodes.release();
+    r->tris.release();
+    r->mats.release();
+    r->counter.release();
+    if (r->ev_start) (void)hipEventDestroy(r->ev_start);
+    if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+    return RT_OK;
+}
+
+int rt_get_params(const rt_renderer* r, rt_params* out) {
+    if (!r || !out) return fail(RT_ERR_ARG, "rt_get_params: null");
+    *out = r->params;
+    return RT_OK;
+}
+
+int rt_set_params(rt_renderer* r, const rt_params* p) {
+    if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
+    if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
+    const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
+    const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
+    r->params = *p;
+    if (rows_changed) {
+        r->frame_count = 0;
+        int rc = zero_image(r);
+        if (rc) return rc;
+    }
+    if (slots_changed && r->sph_geo.ptr) return upload_spheres(r);
+    return RT_OK;
+}
+
+int rt_set_camera(rt_renderer* r, const void* camera80) {
+    if (!r || !camera80) return fail(RT_ERR_ARG, "rt_set_camera: null");
+    std::memcpy(&r->camera, camera80, sizeof(hrt::Camera));
+    r->has_camera = true;
+    return RT_OK;
+}
+
+int rt_set_spheres(rt_renderer* r, const void* spheres48, uint32_t n) {
+    if (!r || (n && !spheres48)) return fail(RT_ERR_ARG, "rt_set_spheres: null");
+    r->spheres.resize(n);
+    if (n) std::memcpy(r->spheres.data(), spheres48, (size_t)n * sizeof(hrt::Sphere));
+    return upload_spheres(r);
+}
+
+int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uint32_t n_nodes, const void* tris64,
+               uint32_t n_tris, const void* mats32, uint32_t n_mats) {
+    if (!r || !sizes) return fail(RT_ERR_ARG, "rt_set_bvh: null");
+    const uint32_t n = sizes[0], m = sizes[1];
+    // The kernel reads nodes[i] for i < n and triangles[j] for j < m only; validate so it cannot fault.
+    if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
+    if ((n && !nodes32) || (m && !tris64) || (n_mats && !mats32)) return fail(RT_ERR_ARG, "rt_set_bvh: null buffer");
+    if (n > (1u << 30)) return fail(RT_ERR_ARG, "rt_set_bvh: tree too large");
+    const hrt::Triangle* T = (const hrt::Triangle*)tris64;
+    std::vector<hrt_dev::TriDev> td(m);
+    for (uint32_t j = 0; j < m; j++) {
+        const hrt::Triangle& t = T[j];
+        if (t.material >= n_mats) return fail(RT_ERR_ARG, "rt_set_bvh: triangle material index out of range");
+        hrt_dev::TriDev d;
+        d.a = float4{t.a.x, t.a.y, t.a.z, 0.0f};
+        d.e1 = float4{t.b.x - t.a.x, t.b.y - t.a.y, t.b.z - t.a.z, 0.0f};  // edge1 = b - a
+        d.e2 = float4{t.c.x - t.a.x, t.c.y - t.a.y, t.c.z - t.a.z, 0.0f};  // edge2 = c - a
+        d.nx = t.custom.x;
+        d.ny = t.custom.y;
+        d.nz = t.custom.z;
+        d.material = t.material;
+        td[j] = d;
+    }
+    const hrt::Material* M = (const hrt::Material*)mats32;
+    std::vector<hrt_dev::MatDev> md(n_mats);
+    for (uint32_t k = 0; k < n_mats; k++)
+        md[k] = hrt_dev::MatDev{M[k].albedo.x, M[k].albedo.y, M[k].albedo.z, M[k].params.x, M[k].kind, 0, 0, 0};
+    int rc = ensure(r->nodes, 2 * (size_t)std::max<uint32_t>(n, 1));
+    if (!rc) rc = ensure(r->tris, std::max<uint32_t>(m, 1));
+    if (!rc) rc = ensure(r->mats, std::max<uint32_t>(n_mats, 1));
+    if (rc) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(r->nodes.ptr, nodes32, (size_t)n * 32u, hipMemcpyHostToDevice, r->stream));
+    if (m) HIP_TRY(hipMemcpyAsync(r->tris.ptr, td.data(), (size_t)m * sizeof(td[0]), hipMemcpyHostToDevice, r->stream));
+    if (n_mats)
+        HIP_TRY(hipMemcpyAsync(r->mats.ptr, md.data(), (size_t)n_mats * sizeof(md[0]), hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    r->bvh_n = n;
+    r->bvh_m = m;
+    return RT_OK;
+}
+
+int rt_set_time(rt_renderer* r, uint32_t time) {
+    if (!r) return fail(RT_ERR_ARG, "rt_set_time: null");
+    r->time = time;
+    return RT_OK;
+}
+
+int rt_set_frame_count(rt_renderer* r, uint32_t fc) {
+    if (!r) return fail(RT_ERR_ARG, "rt_set_frame_count: null");
+    r->frame_count = fc;
+    return RT_OK;
+}
+
+int rt_get_frame_count(const rt_renderer* r, uint32_t* out) {
+    if (!r || !out) return fail(RT_ERR_ARG, "rt_get_frame_count: null");
+    *out = r->frame_count;
+    return RT_OK;
+}
+
+int rt_draw(rt_renderer* r) {
+    if (!r) return fail(RT_ERR_ARG, "rt_draw: null");
+    return launch_frames(r, 1, r->time, 0);
+}
+
+int rt_draw_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime) {
+    if (!r) return fail(RT_ERR_ARG, "rt_draw_frames: null");
+    if (count == 0) return RT_OK;
+    int rc = launch_frames(r, count, time0, dtime);
+    if (!rc) r->time = time0 + (count - 1) * dtime;
+    return rc;
+}
+
+int rt_read_image(rt_renderer* r, float* out, size_t n_floats) {
+    if (!r || !out) return fail(RT_ERR_ARG, "rt_read_image: null");
+    if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_read_image: size mismatch");
+    HIP_TRY(hipMemcpyAsync(out, r->image.ptr, n_floats * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return finish_stats(r);
+}
+
+int rt_write_image(rt_renderer* r, const float* in, size_t n_floats) {
+    if (!r || !in) return fail(RT_ERR_ARG, "rt_write_image: null");
+    if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_write_image: size mismatch");
+    HIP_TRY(hipMemcpyAsync(r->image.ptr, in, n_floats * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+int rt_copy_image_to_device(rt_renderer* r, void* dst, size_t n_floats) {
+    if (!r || !dst) return fail(RT_ERR_ARG, "rt_copy_image_to_device: null");
+    if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_copy_image_to_device: size mismatch");
+    HIP_TRY(hipMemcpyAsync(dst, r->image.ptr, n_floats * sizeof(float), hipMemcpyDeviceToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return finish_stats(r);
+}
+
+int rt_reset_frame_count(rt_renderer* r) {
+    if (!r) return fail(RT_ERR_ARG, "rt_reset_frame_count: null");
+    r->frame_count = 0;
+    return zero_image(r);
+}
+
+int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
+    if (!r) return fail(RT_ERR_ARG, "rt_resize: null");
+    r->width = std::max<uint32_t>(1, width);  // renderer.rs:274-275
+    r->height = std::max<uint32_t>(1, height);
+    if (r->params.row0 >= r->height) r->params.row0 = 0;
+    r->frame_count = 0;
+    return zero_image(r);
+}
+
+int rt_synchronize(rt_renderer* r) {
+    if (!r) return fail(RT_ERR_ARG, "rt_synchronize: null");
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return finish_stats(r);
+}
+
+int rt_get_stats(const rt_renderer* r, rt_stats* out) {
+    if (!r || !out) return fail(RT_ERR_ARG, "rt_get_stats: null");
+    int rc = finish_stats(const_cast<rt_renderer*>(r));
+    if (rc) return rc;
+    *out = r->stats;
+    return RT_OK;
+}
+
+}  // extern "C"

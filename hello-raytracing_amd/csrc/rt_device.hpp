@@ -1,0 +1,120 @@
+// rt_device.hpp — device-side data layout and math of the MI355X path tracer (gfx950).
+//
+// Every formula restates the reference WGSL (hucancode/hello-raytracing src/shaders/shader_sphere.wgsl,
+// shader_tris.wgsl) under the build's float contract, which the CPU oracle
+// follows independently:
+//   * IEEE f32, no contraction (compiled with -ffp-contract=off), denormals kept, correctly rounded
+//     division and sqrt (HIP default -fhip-fp32-correctly-rounded-divide-sqrt);
+//   * fused multiply-add ONLY in dot products (x*x', fma y, fma z [, fma w]), in the sphere
+//     discriminant fma(b, b, -(4a*c)) and in point_on_ray fma(t, d, o);
+//   * normalize(v) = v / sqrt(dot(v, v)); pow(x, 5) = ((x*x)*(x*x))*x; min/max = IEEE minNum/maxNum.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hrt_dev {
+
+constexpr float FLT_MAX_REF = 3.40282e+38f;  // shader_*.wgsl:4
+constexpr int MODE_SPHERE = 0, MODE_TRIS = 1, MODE_MIXED = 2;
+
+// Winner-only sphere data (loaded once per query, for the closest sphere).
+struct SphereAux {
+    float cx, cy, cz, radius;
+    float ar, ag, ab, param;  // albedo.rgb, params.x
+    uint32_t id, pad0, pad1, pad2;
+};
+static_assert(sizeof(SphereAux) == 48, "SphereAux");
+
+// Triangle as the kernel reads it: a, e1 = b - a, e2 = c - a (host-precomputed with the same f32
+// subtraction Moller-Trumbore performs, shader_tris.wgsl:168-169), stored normal + material index.
+struct TriDev {
+    float4 a;   // a.xyz, unused
+    float4 e1;  // (b - a).xyz, unused
+    float4 e2;  // (c - a).xyz, unused
+    float nx, ny, nz;
+    uint32_t material;
+};
+static_assert(sizeof(TriDev) == 64, "TriDev");
+
+struct MatDev {
+    float ar, ag, ab, param;
+    uint32_t id, pad0, pad1, pad2;
+};
+static_assert(sizeof(MatDev) == 32, "MatDev");
+
+// Kernel arguments (passed by value in the kernarg segment).
+struct KParams {
+    float eye[4], dir[4], up[4], right[4];
+    float focal, blur, k;         // k = tan(fov / 2), host libm tanf
+    float aspect, wm1, hm1;       // f32(W)/f32(H), f32(W) - 1, f32(H) - 1 (host, same IEEE ops)
+    uint32_t W, H;
+    uint32_t time0, dtime, frame0, nframes;
+    uint32_t bounces;
+    float ema_cap;                // f32(SAMPLE_FRAME)
+    uint32_t nslots;              // sphere slots scanned (arrayLength semantics)
+    uint32_t n, m;                // bvh_tree_size
+    uint32_t row0, row_step, nrows;
+    float* image;                 // nrows x W x 3
+    const float4* sph_geo;        // (cx, cy, cz, r*r) per slot
+    const SphereAux* sph_aux;     // per slot
+    const float4* nodes;          // 2 float4 per node: min, max
+    const TriDev* tris;
+    const MatDev* mats;
+    unsigned long long* counter;  // closest-hit queries
+};
+
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 a) {
+    float l = length(a);
+    return mk(a.x / l, a.y / l, a.z / l);
+}
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ f3 point_on_ray(f3 o, f3 d, float t) {
+    return mk(__builtin_fmaf(t, d.x, o.x), __builtin_fmaf(t, d.y, o.y), __builtin_fmaf(t, d.z, o.z));
+}
+__device__ __forceinline__ float fmin_ieee(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float fmax_ieee(float a, float b) { return __builtin_fmaxf(a, b); }
+
+// PCG hash step — shader_sphere.wgsl:87-93.
+__device__ __forceinline__ uint32_t pcg_next(uint32_t s) {
+    uint32_t old = s + 747796405u + 2891336453u;
+    uint32_t word = ((old >> ((old >> 28u) + 4u)) ^ old) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+// rng_float — :94-97: f32(state) / f32(0xffffffff) = round(state) * 2^-32.
+__device__ __forceinline__ float rng_float(uint32_t& s) {
+    s = pcg_next(s);
+    return (float)s * 2.3283064365386963e-10f;
+}
+
+// reflect / refract / reflectance — shader_sphere.wgsl:156-171.
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - (2.0f * dot(v, n)) * n; }
+__device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {
+    float cos_t = fmin_ieee(dot(-uv, n), 1.0f);
+    f3 perp = e * (uv + cos_t * n);
+    float len = length(perp);
+    f3 par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len * len))) * n;
+    return perp + par;
+}
+__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {
+    float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+    r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    float x2 = x * x;
+    return r0 + (1.0f - r0) * ((x2 * x2) * x);
+}
+
+}  // namespace hrt_dev

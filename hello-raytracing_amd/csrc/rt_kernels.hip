@@ -1,0 +1,323 @@
+// rt_kernels.hip — the per-pixel path-tracing loop for MI355X (gfx950), hand-written HIP.
+//
+// Replaces the reference's WGSL fragment program fs_main (hucancode/hello-raytracing
+// src/shaders/shader_sphere.wgsl:251-273, shader_tris.wgsl:325-347) run once per pixel per frame by
+// a full-screen draw (src/renderer.rs:382-399). Design:
+//   * one thread per pixel; a wave64 covers an 8x8 pixel tile (ray coherence for the wave-uniform
+//     sphere scan), a 256-thread workgroup a 16x16 tile;
+//   * F frames (samples) per launch, looped IN the kernel: the accumulation (WGSL mix, :264-271) runs
+//     in registers and the framebuffer is read once and written once per launch;
+//   * the bounce loop is flattened into a per-lane query loop: each iteration is ONE closest-hit query
+//     for every live lane; a lane whose path ends (miss or bounce cap) accumulates and immediately
+//     starts its next frame's primary ray, so lanes never idle waiting for the wave's longest path
+//     (lane-level refill instead of wave-level compaction);
+//   * the sphere list is scanned in slot order with a wave-uniform index, so the per-sphere data are
+//     scalar (SGPR) loads shared by the 64 lanes; only the winning sphere's record is gathered;
+//   * the implicit-heap BVH walk (shader_tris.wgsl:268-301) is per lane, with the reference's
+//     traversal order and 600-step cap.
+#include "rt_device.hpp"
+
+using namespace hrt_dev;
+
+namespace {
+
+struct Ray {
+    f3 o, d;
+};
+
+struct Hit {
+    f3 p, n;
+    float t;
+    float ar, ag, ab, param;
+    uint32_t id;
+    bool front;
+};
+
+// intersect_all_sphere + intersect_sphere (shader_sphere.wgsl:218-229, :136-155). Returns the slot of
+// the closest root with t > 0 && t < best (first slot wins ties), or -1. Skipping b >= 0 is exact:
+// then -b - sqrt(disc) <= 0, so t <= 0 (or NaN) and the reference rejects it too.
+__device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, float& best) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    int bi = -1;
+    const float4* __restrict__ geo = P.sph_geo;
+    const uint32_t ns = P.nslots;
+    for (uint32_t i = 0; i < ns; i++) {
+        const float4 g = geo[i];  // wave-uniform: scalar load
+        const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
+        const float b = 2.0f * __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+        const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
+        const float disc = __builtin_fmaf(b, b, -(a4 * c));
+        if (disc >= 0.0f && b < 0.0f) {
+            const float t = (-b - __builtin_sqrtf(disc)) / a2;
+            if (t > 0.0f && t < best) {
+                best = t;
+                bi = (int)i;
+            }
+        }
+    }
+    return bi;
+}
+
+__device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
+    const SphereAux s = P.sph_aux[bi];
+    const f3 p = point_on_ray(r.o, r.d, t);
+    f3 n = p - mk(s.cx, s.cy, s.cz);
+    n = mk(n.x / s.radius, n.y / s.radius, n.z / s.radius);
+    const bool front = dot(r.d, n) < 0.0f;
+    if (!front) n = -n;
+    h.p = p;
+    h.n = n;
+    h.t = t;
+    h.ar = s.ar; h.ag = s.ag; h.ab = s.ab; h.param = s.param;
+    h.id = s.id;
+    h.front = front;
+}
+
+// intersect_node (shader_tris.wgsl:150-159); inv = 1/d is the same value for every node of a query.
+__device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3& o, const f3& inv) {
+    const float4 mn = P.nodes[2 * i];
+    const float4 mx = P.nodes[2 * i + 1];
+    const float t0x = (mn.x - o.x) * inv.x, t0y = (mn.y - o.y) * inv.y, t0z = (mn.z - o.z) * inv.z;
+    const float t1x = (mx.x - o.x) * inv.x, t1y = (mx.y - o.y) * inv.y, t1z = (mx.z - o.z) * inv.z;
+    const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmin_ieee(t0z, t1z));
+    const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmax_ieee(t0z, t1z));
+    return tmin <= tmax && tmax >= 0.0f;
+}
+
+// intersect_triangle, Moller-Trumbore (shader_tris.wgsl:161-202). Updates h when t in [1e-4, h.t).
+__device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_t j, Hit& h) {
+    const TriDev tr = P.tris[j];
+    const f3 e1 = mk(tr.e1.x, tr.e1.y, tr.e1.z);
+    const f3 e2 = mk(tr.e2.x, tr.e2.y, tr.e2.z);
+    const f3 hh = cross(r.d, e2);
+    const float det = dot(e1, hh);
+    if (__builtin_fabsf(det) < 1e-4f) return;
+    const float inv_det = 1.0f / det;
+    const f3 s = r.o - mk(tr.a.x, tr.a.y, tr.a.z);
+    const float u = inv_det * dot(s, hh);
+    if (u < 0.0f || u > 1.0f) return;
+    const f3 q = cross(s, e1);
+    const float v = inv_det * dot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return;
+    const float t = inv_det * dot(e2, q);
+    if (t < 1e-4f || t >= h.t) return;
+    const MatDev m = P.mats[tr.material];
+    h.p = point_on_ray(r.o, r.d, t);
+    h.n = mk(tr.nx, tr.ny, tr.nz);
+    h.t = t;
+    h.ar = m.ar; h.ag = m.ag; h.ab = m.ab; h.param = m.param;
+    h.id = m.id;
+    h.front = dot(h.n, r.d) > 0.0f;
+}
+
+// intersect_all_node (shader_tris.wgsl:268-301): stackless DFS over the implicit heap, 600-step cap.
+__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h) {
+    const f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const uint32_t n = P.n, m = P.m;
+    uint32_t i = 1;
+    for (int step = 0; step < 600; step++) {
+        if (i < n && node_hit(P, i, r.o, inv)) {
+            i *= 2u;
+            continue;
+        }
+        if (i >= n) {
+            const uint32_t j = i - n;
+            if (j >= m) break;
+            tri_test(P, r, j, h);
+        }
+        i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
+        if (i == 0u) break;
+        i++;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h) {
+    h.t = FLT_MAX_REF;
+    if (MODE != MODE_TRIS) {
+        float best = FLT_MAX_REF;
+        const int bi = scan_spheres(P, r, best);
+        if (bi >= 0) sphere_record(P, r, bi, best, h);
+    }
+    if (MODE != MODE_SPHERE) walk_bvh(P, r, h);
+    // abs(hit.t - FLT_MAX) < EPSILON (shader_sphere.wgsl:235): t is FLT_MAX_REF exactly or >= 2^103 away.
+    return h.t != FLT_MAX_REF;
+}
+
+// random_on_hemisphere (shader_sphere.wgsl:107-117): normalised vector in the +++ octant, flipped to n's side.
+template <int MODE>
+__device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
+    constexpr float EPS = MODE == MODE_SPHERE ? 1e-6f : 1e-4f;
+    const float x = rng_float(s);
+    const float y = rng_float(s);
+    const float z = rng_float(s);
+    const f3 v = normalize(mk(x, y, z));
+    if (length(v) < EPS) return n;
+    if (dot(v, n) > 0.0f) return v;
+    return -v;
+}
+
+// scatter (shader_sphere.wgsl:172-217; shader_tris.wgsl:222-267 reflects the raw direction for metal).
+template <int MODE>
+__device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
+    f3 d;
+    if (h.id == 1u) {
+        d = random_on_hemisphere<MODE>(s, h.n);
+    } else if (h.id == 2u) {
+        const f3 in = MODE == MODE_SPHERE ? normalize(r.d) : r.d;
+        const f3 refl = reflect(in, h.n);
+        const f3 hemi = random_on_hemisphere<MODE>(s, h.n);
+        d = normalize(refl + h.param * hemi);
+    } else {  // MAT_DIELECTRIC and the default arm
+        float ir = h.param;
+        if (h.front) ir = 1.0f / ir;
+        const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
+        const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        bool refl = ir * sin_t > 1.0f;  // cannot_refract; WGSL || short-circuits the RNG draw
+        if (!refl) {
+            const float f = rng_float(s);
+            refl = reflectance(cos_t, ir) > (f - __builtin_floorf(f));
+        }
+        d = refl ? normalize(reflect(r.d, h.n)) : normalize(refract(r.d, h.n, ir));
+    }
+    r.o = h.p;
+    r.d = d;
+}
+
+// fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
+template <int MODE>
+__device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
+    s = (x * P.H + y) * time;
+    const float r1 = rng_float(s);
+    const float r2 = rng_float(s);
+    const float l = __builtin_sqrtf(__builtin_fmaf(r2, r2, r1 * r1));
+    const float px = ((float)x + 0.5f) + r1 / l;
+    const float py = ((float)y + 0.5f) + r2 / l;
+    const float ux = (2.0f * (px / P.wm1) - 1.0f) * P.aspect;
+    const float uy = (2.0f * (py / P.hm1) - 1.0f) * -1.0f;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = ((P.right[i] * ux) * P.k + (P.up[i] * uy) * P.k) + P.dir[i];
+    const float lv = __builtin_sqrtf(__builtin_fmaf(v[3], v[3], __builtin_fmaf(v[2], v[2], __builtin_fmaf(v[1], v[1], v[0] * v[0]))));
+    float f4[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) f4[i] = P.eye[i] + (v[i] / lv) * P.focal;
+    // random_on_disk (:118-122): +x,+y quadrant unit vector times rng*radius, in world xy.
+    const float q1 = rng_float(s);
+    const float q2 = rng_float(s);
+    const float lq = __builtin_sqrtf(__builtin_fmaf(q2, q2, q1 * q1));
+    const float rr = rng_float(s) * P.blur;
+    float o4[4];
+    o4[0] = P.eye[0] + (q1 / lq) * rr;
+    o4[1] = P.eye[1] + (q2 / lq) * rr;
+    o4[2] = P.eye[2] + 0.0f * rr;
+    o4[3] = P.eye[3] + 1.0f;
+    Ray r;
+    r.o = mk(o4[0], o4[1], o4[2]);
+    if (MODE == MODE_SPHERE) {
+        r.d = mk(f4[0] - o4[0], f4[1] - o4[1], f4[2] - o4[2]);
+    } else {
+        float g[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) g[i] = f4[i] - o4[i];
+        const float lg = __builtin_sqrtf(__builtin_fmaf(g[3], g[3], __builtin_fmaf(g[2], g[2], __builtin_fmaf(g[1], g[1], g[0] * g[0]))));
+        r.d = mk(g[0] / lg, g[1] / lg, g[2] / lg);
+    }
+    return r;
+}
+
+}  // namespace
+
+// One launch = P.nframes frames over this renderer's rows. Grid: (ceil(W/16), ceil(nrows/16)).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_render(const KParams P) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const bool valid = x < P.W && kr < P.nrows;
+    const uint32_t y = P.row0 + kr * P.row_step;
+    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
+
+    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
+    if (valid) {
+        acc0 = px[0];
+        acc1 = px[1];
+        acc2 = px[2];
+    }
+    uint32_t f = valid ? 0u : P.nframes;
+    uint32_t queries = 0;
+
+    // Path state of the lane's current sample.
+    Ray ray;
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    float sky_t = 0.0f;
+    uint32_t s = 0, bounce = 0;
+    if (f < P.nframes) {
+        ray = primary_ray<MODE>(P, x, y, P.time0, s);
+        sky_t = ray.d.y * 0.5f + 0.5f;
+    }
+
+    while (f < P.nframes) {
+        bool done = true;
+        if (bounce < P.bounces) {
+            Hit h;
+            const bool hit = closest_hit<MODE>(P, ray, h);
+            queries++;
+            if (hit) {
+                scatter<MODE>(s, ray, h);
+                att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                bounce++;
+                done = bounce >= P.bounces;
+            }
+        }
+        if (done) {
+            // trace() epilogue (:241-242) + accumulation (:264-271).
+            const float u = 1.0f - sky_t;
+            const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+            const f3 c = att * sky;
+            const float fc = (float)(P.frame0 + f);
+            const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
+            const float omw = 1.0f - w;
+            acc0 = acc0 * omw + (0.0f + c.x) * w;
+            acc1 = acc1 * omw + (0.0f + c.y) * w;
+            acc2 = acc2 * omw + (0.0f + c.z) * w;
+            f++;
+            if (f < P.nframes) {
+                ray = primary_ray<MODE>(P, x, y, P.time0 + f * P.dtime, s);
+                sky_t = ray.d.y * 0.5f + 0.5f;
+                att = mk(1.0f, 1.0f, 1.0f);
+                bounce = 0;
+            }
+        }
+    }
+
+    if (valid) {
+        px[0] = acc0;
+        px[1] = acc1;
+        px[2] = acc2;
+    }
+    // One atomic per wave for the ray count.
+    unsigned long long qsum = queries;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) qsum += __shfl_xor(qsum, off);
+    if (lane == 0 && qsum) atomicAdd(P.counter, qsum);
+}
+
+template __global__ void k_render<MODE_SPHERE>(const KParams);
+template __global__ void k_render<MODE_TRIS>(const KParams);
+template __global__ void k_render<MODE_MIXED>(const KParams);
+
+// Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI).
+hipError_t hrt_launch_render(int mode, const KParams& P, hipStream_t stream) {
+    dim3 block(256);
+    dim3 grid((P.W + 15u) / 16u, (P.nrows + 15u) / 16u);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    switch (mode) {
+    case MODE_SPHERE: hipLaunchKernelGGL(k_render<MODE_SPHERE>, grid, block, 0, stream, P); break;
+    case MODE_TRIS: hipLaunchKernelGGL(k_render<MODE_TRIS>, grid, block, 0, stream, P); break;
+    default: hipLaunchKernelGGL(k_render<MODE_MIXED>, grid, block, 0, stream, P); break;
+    }
+    return hipGetLastError();
+}

@@ -1,0 +1,159 @@
+/*
+ * hrt.h — C-ABI of the MI355X-native path tracer (drop-in for hucancode/hello-raytracing's per-pixel ray
+ * loop). Plain pointers, sizes and int status codes; no C++ or torch types cross this boundary.
+ *
+ * Two groups of entry points:
+ *   rt_*  (renderer)  replace the wgpu Renderer + bind-group ABI + WGSL fs_main of the reference
+ *                     (src/renderer.rs, src/shaders/shader_{sphere,tris}.wgsl). Backed by HIP kernels
+ *                     for gfx950; they fail with RT_ERR_DEVICE when no MI355X is present — there is
+ *                     no CPU fallback.
+ *   rt_host_* (scene) host-side builders whose output bytes feed the renderer: Camera::new, Mesh::load_obj,
+ *                     Tree::add_mesh/build, render_ppm, compare_ppm_images. Pure CPU.
+ *
+ * Every input buffer uses the reference's #[repr(C)] bytemuck POD layout byte for byte:
+ *   Camera   80 B  {eye, direction, up, right: vec4<f32>; params: (focal, blur, fov, 0)} src/scene/camera.rs:6-12
+ *   Material 32 B  {albedo: vec4<f32>; params: vec3<f32>; kind: u32}                      src/scene/material.rs:9-13
+ *   Sphere   48 B  {center: vec3<f32>; radius: f32; material: Material}                   src/scene/sphere.rs:6-10
+ *   Node     32 B  {bound_min: vec4<f32>; bound_max: vec4<f32>}                          src/scene/bvh/node.rs:6-9
+ *   Triangle 64 B  {a, b, c: vec4<f32>; custom(normal): vec3<f32>; material: u32}       src/scene/bvh/triangle.rs:7-13
+ * The callee copies every input (caller keeps ownership), as wgpu's queue.write_buffer does
+ * (renderer.rs:350-353). One handle must not be used from two threads at once.
+ */
+#ifndef HRT_H
+#define HRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (the reference panics via unwrap/expect instead, e.g. renderer.rs:64,83,117) ---- */
+#define RT_OK 0
+#define RT_ERR_ARG (-1)      /* null pointer, zero size, bad mode, size mismatch                   */
+#define RT_ERR_DEVICE (-2)   /* no gfx950 device / HIP runtime error                               */
+#define RT_ERR_ALLOC (-3)    /* device or host allocation failed                                   */
+#define RT_ERR_STATE (-4)    /* call out of protocol order (e.g. draw before camera)               */
+#define RT_ERR_PARSE (-5)    /* OBJ parse error (tobj LoadError)                                   */
+#define RT_ERR_COMPARE (-6)  /* compare_ppm_images failed (see rt_host_compare_ppm)                */
+
+/* ---- scene modes: which WGSL program the renderer runs ---- */
+#define RT_MODE_SPHERE 0 /* shader_sphere.wgsl: sphere list, BOUNCE_MAX 10, EPSILON 1e-6             */
+#define RT_MODE_TRIS 1   /* shader_tris.wgsl: implicit-heap BVH of triangles, BOUNCE_MAX 5, EPS 1e-4 */
+#define RT_MODE_MIXED 2  /* build-defined union (tris constants + sphere list), DESIGN.md §Mixed     */
+
+/* Material kinds, src/scene/material.rs:4-6 */
+#define RT_LAMBERTIAN 1u
+#define RT_METAL 2u
+#define RT_DIELECTRIC 3u
+
+#define RT_MAX_OBJECT_IN_SCENE 100u /* scene_sphere.rs:15 — sphere buffer capacity = arrayLength */
+#define RT_SAMPLE_FRAME 1000u        /* shader_*.wgsl SAMPLE_FRAME: EMA cap of the accumulation     */
+
+typedef struct rt_renderer rt_renderer;
+
+/* Runtime knobs that are compile-time constants in the WGSL (shader_sphere.wgsl:3-12). */
+typedef struct rt_params {
+    uint32_t bounces;          /* BOUNCE_MAX; default 10 (sphere) / 5 (tris, mixed)                     */
+    uint32_t ema_cap;          /* SAMPLE_FRAME; default 1000                                          */
+    uint32_t min_sphere_slots; /* arrayLength(&scene) floor; default 100 (zero-filled slots traced)    */
+    uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
+    uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
+} rt_params;
+
+typedef struct rt_stats {
+    uint64_t queries;      /* closest-hit queries (rays) traced by the last draw call                  */
+    uint64_t samples;      /* pixel-samples (pixels x frames) of the last draw call                    */
+    double kernel_ms;      /* HIP-event time of the last draw call's kernels, on the renderer stream   */
+    uint32_t launches;     /* kernel launches of the last draw call                                    */
+    uint32_t local_rows;   /* rows owned by this renderer                                              */
+} rt_stats;
+
+/* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),
+ * frame_count = 0. Selects the program (mode) like include_str!(shader) does (scene_sphere.rs:186). */
+int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer **out);
+int rt_destroy(rt_renderer *r);
+int rt_get_params(const rt_renderer *r, rt_params *out);
+/* Changing row0/row_step re-allocates and zeroes the image (like resize). */
+int rt_set_params(rt_renderer *r, const rt_params *p);
+
+/* Renderer::set_camera — renderer.rs:324-328 (group0 binding 4, 80 B). */
+int rt_set_camera(rt_renderer *r, const void *camera80);
+/* SceneSphere::write_scene_data -> Renderer::write_buffer(data, 0) — scene_sphere.rs:24-31,
+ * renderer.rs:350-353 (group1 binding 0). n spheres of 48 B; slots past n are zero, like the wgpu buffer. */
+int rt_set_spheres(rt_renderer *r, const void *spheres48, uint32_t n);
+/* SceneTris::write_tree_data — scene_tris.rs:21-44 (group1 bindings 0..3): sizes = [n, m] (bvh_tree_size),
+ * n Node (index 0 unused), m Triangle, k Material. */
+int rt_set_bvh(rt_renderer *r, const uint32_t sizes[2], const void *nodes32, uint32_t n_nodes,
+               const void *tris64, uint32_t n_tris, const void *mats32, uint32_t n_mats);
+
+/* Renderer::set_time / set_frame_count — renderer.rs:315-323. */
+int rt_set_time(rt_renderer *r, uint32_t time);
+int rt_set_frame_count(rt_renderer *r, uint32_t frame_count);
+int rt_get_frame_count(const rt_renderer *r, uint32_t *out);
+
+/* Renderer::draw — renderer.rs:355-410: one frame (one sample per pixel) at the current time,
+ * frame_count += 1. Asynchronous on the renderer's HIP stream. */
+int rt_draw(rt_renderer *r);
+/* `count` frames with time_f = time0 + f*dtime, frame_count advancing by one per frame: bit-identical
+ * to count x {rt_set_time(time_f); rt_draw()} (the accumulation runs in registers in-kernel). */
+int rt_draw_frames(rt_renderer *r, uint32_t count, uint32_t time0, uint32_t dtime);
+
+/* render_ppm's copy_image_buffer — render_ppm.rs:7-36: blocking readback of the f32 RGB image,
+ * row-major, (local_rows x width x 3) floats. */
+int rt_read_image(rt_renderer *r, float *out, size_t n_floats);
+/* Restore an accumulation state (checkpoint/resume: image + rt_set_frame_count). */
+int rt_write_image(rt_renderer *r, const float *in, size_t n_floats);
+/* Device-to-device copy of the image into caller memory on the caller's device (multi-GPU gather). */
+int rt_copy_image_to_device(rt_renderer *r, void *dst_device, size_t n_floats);
+/* Renderer::reset_frame_count / resize — renderer.rs:336-348, :271-313 (both zero the image). */
+int rt_reset_frame_count(rt_renderer *r);
+int rt_resize(rt_renderer *r, uint32_t width, uint32_t height);
+int rt_synchronize(rt_renderer *r);
+int rt_get_stats(const rt_renderer *r, rt_stats *out);
+
+/* Thread-local message for the last failing call. */
+const char *rt_last_error(void);
+/* Number of visible gfx950 devices (0 on a CPU-only host; never an error). */
+int rt_device_count(void);
+/* Build string of the device code object ("gfx950 ..."), for the load check. */
+const char *rt_build_info(void);
+
+/* ================================ host-side scene builders ================================ */
+
+/* Camera::new(from, to, focal_length, focal_blur_amount, fov) — src/scene/camera.rs:15-28 (glam 0.24 f32). */
+int rt_host_camera_new(const float from[3], const float to[3], float focal_length, float focal_blur_amount,
+                       float fov, void *camera80_out);
+
+typedef struct rt_mesh rt_mesh;
+typedef struct rt_tree rt_tree;
+
+/* Mesh::load_obj(source, material) — src/geometry/mesh.rs:11-62 (tobj 4.0.3 default LoadOptions).
+ * Like the reference, a parse failure yields an EMPTY mesh (status RT_OK) — see rt_host_mesh_counts. */
+int rt_host_mesh_load_obj(const char *data, size_t len, const void *material32, rt_mesh **out);
+int rt_host_mesh_counts(const rt_mesh *m, uint32_t *n_vertices, uint32_t *n_indices);
+int rt_host_mesh_destroy(rt_mesh *m);
+
+/* Tree::new / Tree::add_mesh / Tree::build — src/scene/bvh/tree.rs:20-90. */
+int rt_host_tree_new(rt_tree **out);
+int rt_host_tree_add_mesh(rt_tree *t, const rt_mesh *m);
+int rt_host_tree_build(rt_tree *t);
+/* Views into the tree (valid until the next mutation): sizes [n, m], n nodes, m triangles, k materials. */
+int rt_host_tree_view(const rt_tree *t, uint32_t sizes[2], const void **nodes32, uint32_t *n_nodes,
+                      const void **tris64, uint32_t *n_tris, const void **mats32, uint32_t *n_mats);
+int rt_host_tree_destroy(rt_tree *t);
+
+/* render_ppm — src/scene/render_ppm.rs:38-57: ASCII P3, `(v*255) as u8` (saturating, truncating,
+ * NaN -> 0). Writes at most cap bytes to out (may be NULL to query); *len = full length. */
+int rt_host_render_ppm(const float *rgb, uint32_t width, uint32_t height, char *out, size_t cap, size_t *len);
+/* compare_ppm_images — tests/rendering_tests.rs:84-131. Returns RT_OK if mean |du8| <= tolerance % of 255;
+ * otherwise RT_ERR_COMPARE with *code = 1 DifferentDimensions, 2 PixelCountMismatch,
+ * 3 ExcessiveDifference. *avg_diff_percent is filled whenever the pixel lists were compared. */
+int rt_host_compare_ppm(const char *img1, size_t len1, const char *img2, size_t len2, float tolerance_percent,
+                        int *code, float *avg_diff_percent);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HRT_H */

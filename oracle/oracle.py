@@ -1,0 +1,97 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/build/liboracle.so (rt_oracle.c).
+
+The CPU restatement of the reference's WGSL ray loop. Imported only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg, as the checker / timed CPU baseline — never by the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "liboracle.so"
+
+MODE_SPHERE, MODE_TRIS, MODE_MIXED = 0, 1, 2
+
+
+class OParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("width", "height", "mode", "bounces", "ema_cap", "frame0", "time0",
+                                          "dtime", "frames", "x0", "nx", "row0", "row_step", "nrows")]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", os.fspath(HERE)], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = C.CDLL(os.fspath(LIB))
+        L.oracle_render.restype = C.c_uint64
+        L.oracle_render.argtypes = [C.POINTER(OParams), C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_sizeof.restype = C.c_uint32
+        L.oracle_sizeof.argtypes = [C.c_int]
+        assert [L.oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
+        _lib = L
+    return _lib
+
+
+def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: int, time0: int = 1000,
+           dtime: int = 10, frame0: int = 0, bounces: int | None = None, ema_cap: int = 1000,
+           spheres: np.ndarray | None = None, min_sphere_slots: int | None = None, bvh=None,
+           rows=None, x0: int = 0, nx: int | None = None, image: np.ndarray | None = None,
+           threads: int = 0):
+    """Render `frames` frames (time0 + f*dtime, frame_count frame0 + f) of a scene.
+
+    spheres: SPHERE_DTYPE array (zero slots appended up to min_sphere_slots, default 100 in sphere mode
+    like the reference's 100-slot buffer); bvh: (sizes, nodes, triangles, materials) from Tree.view().
+    rows: (row0, row_step, nrows) subset of rows (global coordinates), default all rows.
+    Returns (image[nrows, nx, 3] float32, queries).
+    """
+    if bounces is None:
+        bounces = 10 if mode == MODE_SPHERE else 5
+    if min_sphere_slots is None:
+        min_sphere_slots = 100 if mode == MODE_SPHERE else 0
+    row0, row_step, nrows = rows if rows is not None else (0, 1, height)
+    nx = width - x0 if nx is None else nx
+    p = OParams(width, height, mode, bounces, ema_cap, frame0, time0, dtime, frames, x0, nx, row0, row_step, nrows)
+    sph_ptr, nslots, keep = None, 0, []
+    if mode != MODE_TRIS:
+        sp = spheres if spheres is not None else np.zeros(0, dtype=np.uint8)
+        n = len(sp)
+        nslots = max(n, min_sphere_slots)
+        buf = np.zeros(nslots * 48, dtype=np.uint8)
+        if n:
+            buf[: n * 48] = np.frombuffer(np.ascontiguousarray(sp).tobytes(), dtype=np.uint8)
+        keep.append(buf)
+        sph_ptr = buf.ctypes.data
+    sizes_p = nodes_p = tris_p = mats_p = None
+    if mode != MODE_SPHERE and bvh is not None:
+        sizes, nodes, tris, mats = bvh
+        sz = np.array(sizes, dtype=np.uint32)
+        nodes, tris, mats = (np.ascontiguousarray(a) for a in (nodes, tris, mats))
+        keep += [sz, nodes, tris, mats]
+        sizes_p, nodes_p, tris_p, mats_p = sz.ctypes.data, nodes.ctypes.data, tris.ctypes.data, mats.ctypes.data
+    elif mode != MODE_SPHERE:
+        sz = np.zeros(2, dtype=np.uint32)
+        keep.append(sz)
+        sizes_p = sz.ctypes.data
+    if image is None:
+        image = np.zeros((nrows, nx, 3), dtype=np.float32)
+    else:
+        image = np.ascontiguousarray(image, dtype=np.float32).copy()
+        assert image.shape == (nrows, nx, 3)
+    cam = np.ascontiguousarray(camera).tobytes()
+    q = lib().oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
+                            image.ctypes.data, threads)
+    return image, int(q)

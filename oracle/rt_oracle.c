@@ -1,0 +1,353 @@
+/*
+ * rt_oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of the reference's per-pixel ray loop.
+ *
+ * This file is the parity oracle (and the timed "port" CPU baseline) for the MI355X path tracer in
+ * hello-raytracing_amd/. It restates, statement by statement, the two WGSL fragment shaders of
+ * hucancode/hello-raytracing:
+ *     src/shaders/shader_sphere.wgsl   (sphere list, BOUNCE_MAX = 10, EPSILON = 1e-6)
+ *     src/shaders/shader_tris.wgsl     (implicit-heap BVH + triangles, BOUNCE_MAX = 5, EPSILON = 1e-4)
+ * plus the frame protocol of src/renderer.rs (frame_count / time uniforms, :315-323, :355-410).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code, and only as
+ * the checker. The product (hello-raytracing_amd/) never includes, links or calls it.
+ *
+ * Pinning: the reference is Rust + WGSL run through wgpu; there is no Rust toolchain, no wgpu and no
+ * GPU here, so it cannot be built. This restatement is pinned by the reference's
+ * own golden images (tests/rendering_tests.rs:134-509, tests/golden/*.ppm): >= 99.9 % of u8 channels
+ * bit-exact on the five non-glass scenes, harness metric (mean |du8| <= 2 % of 255) on all seven.
+ * The triangle/BVH path has no image golden in the reference: it is pinned structurally only
+ * (bvh/tree.rs:93-126) — "parity unpinned" at image level for tris mode.
+ *
+ * Float semantics (build-defined, documented in DESIGN.md §Numerics; the HIP kernels follow the same
+ * rules, written independently):
+ *   - IEEE f32, round-to-nearest, no contraction (compile with -ffp-contract=off), denormals kept;
+ *   - fused multiply-add in exactly three places: dot products (x*x' then fma(y), fma(z)[, fma(w)]),
+ *     the sphere discriminant fma(b, b, -(4a*c)), and point_on_ray fma(t, d, o);
+ *   - normalize(v) = v / sqrt(dot(v, v)) component-wise; division and sqrt correctly rounded;
+ *   - pow(x, 5.0) = ((x*x)*(x*x))*x;  min/max = fminf/fmaxf (IEEE minNum/maxNum);
+ *   - tan(fov/2) by libm tanf (the device path receives the same host-computed value).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define FLT_MAX_REF 3.40282e+38f /* shader_*.wgsl:4 */
+
+enum { MODE_SPHERE = 0, MODE_TRIS = 1, MODE_MIXED = 2 };
+
+/* ---- reference POD layouts (bytemuck #[repr(C)]), src/scene/{camera,material,sphere}.rs, bvh/ ---- */
+typedef struct { float eye[4], dir[4], up[4], right[4], params[4]; } o_camera;          /* 80 B */
+typedef struct { float albedo[4]; float params[3]; uint32_t id; } o_material;              /* 32 B */
+typedef struct { float center[3]; float radius; o_material mat; } o_sphere;                /* 48 B */
+typedef struct { float bmin[4]; float bmax[4]; } o_node;                                   /* 32 B */
+typedef struct { float a[4], b[4], c[4]; float normal[3]; uint32_t material; } o_triangle; /* 64 B */
+
+typedef struct {
+    uint32_t width, height;   /* resolution uniform (renderer.rs:242-247)                       */
+    uint32_t mode;            /* MODE_*                                                          */
+    uint32_t bounces;         /* BOUNCE_MAX (10 sphere / 5 tris in the reference)                */
+    uint32_t ema_cap;         /* SAMPLE_FRAME (1000)                                             */
+    uint32_t frame0;          /* frame_count of the first frame drawn                            */
+    uint32_t time0, dtime;    /* time of frame f = time0 + f*dtime (tests: 1000 + 10 i)          */
+    uint32_t frames;          /* frames drawn by this call                                       */
+    uint32_t x0, nx;          /* column window                                                   */
+    uint32_t row0, row_step, nrows; /* rows row0 + k*row_step, k < nrows                         */
+} o_params;
+
+typedef struct { float x, y, z; } v3;
+static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
+static inline v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
+static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
+static inline v3 norm3(v3 a) { float l = len3(a); return V(a.x / l, a.y / l, a.z / l); }
+static inline v3 cross3(v3 a, v3 b) {
+    return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline v3 ld3(const float *p) { return V(p[0], p[1], p[2]); }
+
+/* rng_int / rng_float / rng_vec2 / rng_vec3: shader_sphere.wgsl:87-103 (= shader_tris.wgsl:99-115) */
+static inline void rng_int(uint32_t *s) {
+    uint32_t old = *s + 747796405u + 2891336453u;
+    uint32_t word = ((old >> ((old >> 28u) + 4u)) ^ old) * 277803737u;
+    *s = (word >> 22u) ^ word;
+}
+static inline float rng_float(uint32_t *s) { rng_int(s); return (float)(*s) / 4294967296.0f; }
+static inline v3 rng_vec3(uint32_t *s) {
+    float x = rng_float(s); float y = rng_float(s); float z = rng_float(s);
+    return V(x, y, z);
+}
+
+typedef struct { v3 o, d; } ray_t;
+typedef struct { v3 p, n; float t; const o_material *mat; int front; } hit_t;
+
+typedef struct {
+    const o_camera *cam; float k;            /* k = tan(fov*0.5) */
+    const o_sphere *spheres; uint32_t nslots;
+    const o_node *nodes; const o_triangle *tris; const o_material *mats; uint32_t n, m;
+    uint32_t mode, bounces; float eps;
+} o_scene;
+
+/* random_on_hemisphere: shader_sphere.wgsl:107-117 / shader_tris.wgsl:119-128 */
+static inline v3 random_on_hemisphere(uint32_t *s, v3 n, float eps) {
+    v3 v = norm3(rng_vec3(s));
+    if (len3(v) < eps) return n;
+    if (dot3(v, n) > 0.0f) return v;
+    return vneg(v);
+}
+
+/* make_ray: shader_sphere.wgsl:123-135 (direction not normalised) / shader_tris.wgsl:136-148 */
+static ray_t make_ray(const o_scene *sc, float ux, float uy, uint32_t *s) {
+    const o_camera *c = sc->cam;
+    float v[4], d4[4], f4[4], o4[4];
+    for (int i = 0; i < 4; i++) {
+        float xx = (c->right[i] * ux) * sc->k;
+        float yy = (c->up[i] * uy) * sc->k;
+        v[i] = (xx + yy) + c->dir[i];
+    }
+    float l = sqrtf(fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0]))));
+    for (int i = 0; i < 4; i++) d4[i] = v[i] / l;
+    for (int i = 0; i < 4; i++) f4[i] = c->eye[i] + d4[i] * c->params[0];
+    /* random_on_disk: shader_sphere.wgsl:118-122 */
+    float r1 = rng_float(s), r2 = rng_float(s);
+    float l2 = sqrtf(fmaf(r2, r2, r1 * r1));
+    float vx = r1 / l2, vy = r2 / l2;
+    float rr = rng_float(s) * c->params[1];
+    o4[0] = c->eye[0] + vx * rr;
+    o4[1] = c->eye[1] + vy * rr;
+    o4[2] = c->eye[2] + 0.0f * rr;
+    o4[3] = c->eye[3] + 1.0f;
+    ray_t r;
+    r.o = V(o4[0], o4[1], o4[2]);
+    if (sc->mode == MODE_SPHERE) {
+        r.d = V(f4[0] - o4[0], f4[1] - o4[1], f4[2] - o4[2]);
+    } else {
+        float g[4];
+        for (int i = 0; i < 4; i++) g[i] = f4[i] - o4[i];
+        float lg = sqrtf(fmaf(g[3], g[3], fmaf(g[2], g[2], fmaf(g[1], g[1], g[0] * g[0]))));
+        r.d = V(g[0] / lg, g[1] / lg, g[2] / lg);
+    }
+    return r;
+}
+
+/* intersect_all_sphere + intersect_sphere: shader_sphere.wgsl:218-229, :136-155.
+ * Closest accepted root over ALL slots (arrayLength = buffer capacity, zero-filled past N). */
+static void closest_sphere(const o_scene *sc, ray_t r, hit_t *h) {
+    float a = dot3(r.d, r.d);
+    float best = h->t;
+    int idx = -1;
+    for (uint32_t i = 0; i < sc->nslots; i++) {
+        const o_sphere *sp = &sc->spheres[i];
+        v3 oc = vsub(r.o, ld3(sp->center));
+        float b = 2.0f * dot3(oc, r.d);
+        float c = dot3(oc, oc) - sp->radius * sp->radius;
+        float disc = fmaf(b, b, -((4.0f * a) * c));
+        if (disc < 0.0f) continue; /* t = -1 */
+        float t = (-b - sqrtf(disc)) / (2.0f * a);
+        if (t > 0.0f && t < best) { best = t; idx = (int)i; }
+    }
+    if (idx < 0) return;
+    const o_sphere *sp = &sc->spheres[idx];
+    v3 p = V(fmaf(best, r.d.x, r.o.x), fmaf(best, r.d.y, r.o.y), fmaf(best, r.d.z, r.o.z));
+    v3 n = vsub(p, ld3(sp->center));
+    n = V(n.x / sp->radius, n.y / sp->radius, n.z / sp->radius);
+    int front = dot3(r.d, n) < 0.0f;
+    if (!front) n = vneg(n);
+    h->p = p; h->n = n; h->t = best; h->mat = &sp->mat; h->front = front;
+}
+
+/* intersect_node: shader_tris.wgsl:150-159 (inv_d hoisted: identical value for every node) */
+static inline int node_hit(v3 o, v3 inv, const o_node *nd) {
+    float t0x = (nd->bmin[0] - o.x) * inv.x, t0y = (nd->bmin[1] - o.y) * inv.y, t0z = (nd->bmin[2] - o.z) * inv.z;
+    float t1x = (nd->bmax[0] - o.x) * inv.x, t1y = (nd->bmax[1] - o.y) * inv.y, t1z = (nd->bmax[2] - o.z) * inv.z;
+    float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    return tmin <= tmax && tmax >= 0.0f;
+}
+
+/* intersect_triangle (Moller-Trumbore): shader_tris.wgsl:161-202 */
+static inline void tri_test(const o_scene *sc, ray_t r, uint32_t j, hit_t *h) {
+    const o_triangle *tr = &sc->tris[j];
+    v3 a = ld3(tr->a), b = ld3(tr->b), c = ld3(tr->c);
+    v3 e1 = vsub(b, a), e2 = vsub(c, a);
+    v3 hh = cross3(r.d, e2);
+    float det = dot3(e1, hh);
+    if (fabsf(det) < 1e-4f) return;
+    float inv_det = 1.0f / det;
+    v3 s = vsub(r.o, a);
+    float u = inv_det * dot3(s, hh);
+    if (u < 0.0f || u > 1.0f) return;
+    v3 q = cross3(s, e1);
+    float v = inv_det * dot3(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return;
+    float t = inv_det * dot3(e2, q);
+    if (t < 1e-4f || t >= h->t) return;
+    h->p = V(fmaf(t, r.d.x, r.o.x), fmaf(t, r.d.y, r.o.y), fmaf(t, r.d.z, r.o.z));
+    h->n = ld3(tr->normal);
+    h->t = t;
+    h->mat = &sc->mats[tr->material];
+    h->front = dot3(h->n, r.d) > 0.0f;
+}
+
+/* intersect_all_node: shader_tris.wgsl:268-301 — stackless walk of the implicit heap, 600-step cap */
+static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h) {
+    v3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    uint32_t i = 1, n = sc->n, m = sc->m;
+    int step = 0;
+    while (step < 600) {
+        step++;
+        if (i < n && node_hit(r.o, inv, &sc->nodes[i])) { i *= 2u; continue; }
+        if (i >= n) {
+            uint32_t j = i - n;
+            if (j >= m) break;
+            tri_test(sc, r, j, h);
+        }
+        while ((i & 1u) == 1u) i /= 2u;
+        if (i == 0u) break;
+        i++;
+    }
+}
+
+static inline v3 reflect3(v3 v, v3 n) { return vsub(v, smul(2.0f * dot3(v, n), n)); }
+static inline v3 refract3(v3 uv, v3 n, float e) { /* shader_sphere.wgsl:159-165 */
+    float cos_t = fminf(dot3(vneg(uv), n), 1.0f);
+    v3 perp = smul(e, vadd(uv, smul(cos_t, n)));
+    float len = len3(perp);
+    v3 par = smul(-sqrtf(fabsf(1.0f - len * len)), n);
+    return vadd(perp, par);
+}
+static inline float reflectance(float cosine, float ref_idx) { /* :166-171, pow(x,5) = x^4*x */
+    float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+    r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    float x2 = x * x;
+    return r0 + (1.0f - r0) * ((x2 * x2) * x);
+}
+
+/* scatter: shader_sphere.wgsl:172-217 / shader_tris.wgsl:222-267 (metal: tris reflects the raw d) */
+static ray_t scatter(const o_scene *sc, uint32_t *s, ray_t r, const hit_t *h) {
+    ray_t out; out.o = h->p;
+    uint32_t id = h->mat->id;
+    if (id == 1u) {
+        out.d = random_on_hemisphere(s, h->n, sc->eps);
+    } else if (id == 2u) {
+        float fuzz = h->mat->params[0];
+        v3 in = sc->mode == MODE_SPHERE ? norm3(r.d) : r.d;
+        v3 refl = reflect3(in, h->n);
+        v3 hemi = random_on_hemisphere(s, h->n, sc->eps);
+        out.d = norm3(vadd(refl, smul(fuzz, hemi)));
+    } else { /* MAT_DIELECTRIC and default */
+        float ir = h->mat->params[0];
+        if (h->front) ir = 1.0f / ir;
+        float cos_t = fminf(dot3(vneg(r.d), h->n), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        int cannot = ir * sin_t > 1.0f;
+        int refl = cannot;
+        if (!refl) { /* WGSL || short-circuits: no RNG draw when cannot_refract */
+            float f = rng_float(s);
+            refl = reflectance(cos_t, ir) > (f - floorf(f));
+        }
+        out.d = refl ? norm3(reflect3(r.d, h->n)) : norm3(refract3(r.d, h->n, ir));
+    }
+    return out;
+}
+
+/* trace: shader_sphere.wgsl:230-243 / shader_tris.wgsl:303-316 */
+static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *queries) {
+    v3 att = V(1.0f, 1.0f, 1.0f);
+    ray_t cur = primary;
+    for (uint32_t b = 0; b < sc->bounces; b++) {
+        hit_t h = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, FLT_MAX_REF, 0, 0};
+        if (sc->mode != MODE_TRIS) closest_sphere(sc, cur, &h);
+        if (sc->mode != MODE_SPHERE) closest_bvh(sc, cur, &h);
+        (*queries)++;
+        if (fabsf(h.t - FLT_MAX_REF) < sc->eps) break;
+        cur = scatter(sc, s, cur, &h);
+        const float *al = h.mat->albedo;
+        att = vmul(att, V(al[0] * 0.7f, al[1] * 0.7f, al[2] * 0.7f));
+    }
+    float tt = primary.d.y * 0.5f + 0.5f;
+    v3 sky = V(0.54f * (1.0f - tt) + 0.54f * tt, 0.86f * (1.0f - tt) + 0.7f * tt, 0.92f * (1.0f - tt) + 0.98f * tt);
+    return vmul(att, sky);
+}
+
+/* fs_main: shader_sphere.wgsl:251-273 — one pixel, one frame */
+static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, uint32_t y, uint32_t time,
+                       uint64_t *queries) {
+    uint32_t s = (x * H + y) * time;
+    float aspect = (float)W / (float)H;
+    float r1 = rng_float(&s), r2 = rng_float(&s);
+    float l = sqrtf(fmaf(r2, r2, r1 * r1));
+    float px = ((float)x + 0.5f) + r1 / l;
+    float py = ((float)y + 0.5f) + r2 / l;
+    float ux = px / ((float)W - 1.0f), uy = py / ((float)H - 1.0f);
+    ux = (2.0f * ux - 1.0f) * aspect;
+    uy = (2.0f * uy - 1.0f) * -1.0f;
+    ray_t r = make_ray(sc, ux, uy, &s);
+    v3 c = trace(sc, r, &s, queries);
+    return V(0.0f + c.x, 0.0f + c.y, 0.0f + c.z);
+}
+
+/*
+ * oracle_render: draw p->frames frames into `image` (rows k < nrows, columns x0..x0+nx, RGB f32,
+ * layout ((k*nx) + (x-x0))*3), continuing the accumulation already in `image` exactly as
+ * repeated Renderer::draw() calls do (renderer.rs:355-410, accumulation at shader_sphere.wgsl:264-271).
+ * Returns the number of closest-hit queries (rays) traced.
+ */
+uint64_t oracle_render(const o_params *p, const void *camera80, const void *spheres48, uint32_t nslots,
+                       const uint32_t *sizes, const void *nodes32, const void *tris64, const void *mats32,
+                       float *image, int threads) {
+    o_scene sc;
+    sc.cam = (const o_camera *)camera80;
+    sc.k = tanf(sc.cam->params[2] * 0.5f);
+    sc.spheres = (const o_sphere *)spheres48; sc.nslots = spheres48 ? nslots : 0;
+    sc.nodes = (const o_node *)nodes32; sc.tris = (const o_triangle *)tris64; sc.mats = (const o_material *)mats32;
+    sc.n = sizes ? sizes[0] : 0; sc.m = sizes ? sizes[1] : 0;
+    sc.mode = p->mode; sc.bounces = p->bounces;
+    sc.eps = p->mode == MODE_SPHERE ? 1e-6f : 1e-4f;
+    uint64_t total = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+#endif
+    for (int64_t k = 0; k < (int64_t)p->nrows; k++) {
+        uint32_t y = p->row0 + (uint32_t)k * p->row_step;
+        uint64_t q = 0;
+        for (uint32_t x = p->x0; x < p->x0 + p->nx; x++) {
+            float *px = image + ((size_t)k * p->nx + (x - p->x0)) * 3;
+            float r = px[0], g = px[1], b = px[2];
+            for (uint32_t f = 0; f < p->frames; f++) {
+                uint32_t fc = p->frame0 + f;
+                uint32_t time = p->time0 + f * p->dtime;
+                v3 c = sample_pixel(&sc, p->width, p->height, x, y, time, &q);
+                float w = 1.0f / (fminf((float)fc, (float)p->ema_cap) + 1.0f);
+                r = r * (1.0f - w) + c.x * w;
+                g = g * (1.0f - w) + c.y * w;
+                b = b * (1.0f - w) + c.z * w;
+            }
+            px[0] = r; px[1] = g; px[2] = b;
+        }
+        total += q;
+    }
+    return total;
+}
+
+/* Size checks so the ctypes wrapper can verify it agrees on the POD layouts. */
+uint32_t oracle_sizeof(int which) {
+    switch (which) {
+    case 0: return sizeof(o_camera);
+    case 1: return sizeof(o_material);
+    case 2: return sizeof(o_sphere);
+    case 3: return sizeof(o_node);
+    case 4: return sizeof(o_triangle);
+    case 5: return sizeof(o_params);
+    default: return 0;
+    }
+}
