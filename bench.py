@@ -1,0 +1,221 @@
+"""Benchmark: Mrays/s of the MI355X path tracer on BASELINE.json's headline workload.
+
+Workload (BASELINE.json metric "Mrays/sec at 1920x1080x1024spp x 50-bounce"): config C3 — the RTIOW-style
+random-spheres cover scene (488 spheres, seeded), 1920x1080, 1024 frames (= spp), 50-bounce cap, sphere
+mode. One STEP = one full render of that image (all 1024 frames, all rows) into a zeroed accumulation
+buffer, scene already resident in HBM. A "ray" is one closest-hit query (primary + every scattered ray,
+terminating miss included), counted exactly by the kernel.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the image is split by
+interleaved rows (rank r renders rows r, r+N, ...: sky-heavy top rows spread evenly), every rank renders
+its rows for all frames, then one RCCL gather over xGMI assembles the full image on rank 0 (inside the
+timed region). Total work is fixed as N grows -> "scaling": "strong"; `value` is the whole-job rate.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), plus `roofline` (FP32-VALU bound; HIP-event
+time of the render kernel on the stream it runs on) and `cpu_baseline` (the CPU oracle on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (ROOT, ROOT / "hello-raytracing_amd", ROOT / "tests"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak with packed FMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+SPHERE_TEST_FLOP = 18  # per ray-sphere test (a, 4a hoisted per query)
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sd, threads: int, rows: int, frames: int):
+    """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload."""
+    import scenes
+
+    H = sd.height
+    step = max(1, H // rows)
+    n = len(range(0, H, step))
+    t0 = time.perf_counter()
+    _, q = scenes.oracle_render(sd, frames=frames, rows=(0, step, n), threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(q / dt / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sd.name}: {n} rows (every {step}th) x {sd.width} px x {frames} frames, {q} rays in {dt:.1f} s",
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=1024, help="spp per step (BASELINE: 1024)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames-per-launch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=24)
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import hrt
+    import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    sd = scenes.config_c3(args.width, args.height, args.frames)
+    nslots = len(sd.spheres)
+    r = scenes.make_renderer(sd)
+    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch)
+    local_rows = r.local_rows
+    max_rows = (sd.height + world - 1) // world
+    part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
+    gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
+    full = torch.empty((sd.height, sd.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def step():
+        r.reset_frame_count()
+        r.draw_frames(sd.frames, 1000, 10)
+        r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
+        st = r.stats()
+        if dist is not None:
+            dist.gather(part, gathered, dst=0)
+            if rank == 0:
+                for k in range(world):
+                    rows_k = len(range(k, sd.height, world))
+                    full[k::world] = gathered[k][:rows_k]
+        elif rank == 0:
+            full.copy_(part[:local_rows])
+        return st
+
+    log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
+        f"{local_rows} rows, warmup {args.warmup}")
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        log(f"warmup {i}: {time.perf_counter() - t:.2f} s")
+
+    barrier()
+    t0 = time.perf_counter()
+    queries = 0
+    kernel_ms = 0.0
+    launches = 0
+    for i in range(args.steps):
+        st = step()
+        queries += st.queries
+        kernel_ms += st.kernel_ms
+        launches += st.launches
+        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernel {st.kernel_ms:.1f} ms")
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        all_t = [torch.zeros_like(stats_t) for _ in range(world)]
+        dist.all_gather(all_t, stats_t)
+        all_t = torch.stack(all_t).cpu().numpy()
+    else:
+        all_t = stats_t.cpu().numpy()[None]
+    t_max = float(all_t[:, 0].max())
+    total_q = float(all_t[:, 1].sum())
+
+    if rank == 0:
+        value = total_q / t_max / 1e6
+        # roofline of the render kernel on rank 0: algorithmic FLOPs per launch / HIP-event launch time
+        my_q, my_ms, my_launches = float(all_t[0, 1]), float(all_t[0, 2]), float(all_t[0, 3])
+        avg_launch_ms = my_ms / max(my_launches, 1.0)
+        flop_per_launch = SPHERE_TEST_FLOP * nslots * my_q / max(my_launches, 1.0)
+        achieved = flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
+        px = local_rows * sd.width
+        alg_bytes = 24.0 * px + 64.0 * nslots  # framebuffer read+write per launch + sphere arrays
+        traffic = None
+        pmc = ROOT / "profiles" / "pmc_summary.json"
+        if pmc.exists():
+            try:
+                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        out = {
+            "metric": "Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded RTIOW-style scene, committed generator tests/scenes.py)",
+            "config": {
+                "workload": sd.name,
+                "width": sd.width,
+                "height": sd.height,
+                "spp": sd.frames,
+                "bounces": sd.bounces,
+                "spheres": nslots,
+                "rays_per_step": round(total_q / args.steps),
+                "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
+                "parallelism": f"rows{world}",
+            },
+            "roofline": {
+                "bound": "fp32-valu",
+                "achieved": round(achieved, 3),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "kernel": "k_render<sphere>",
+                "avg_launch_ms": round(avg_launch_ms, 3),
+                "flop_per_launch": flop_per_launch,
+                "alg_hbm_bytes_per_launch": alg_bytes,
+                "hbm_gbs_alg": round(alg_bytes / (avg_launch_ms * 1e-3) / 1e9, 3),
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            log("cpu baseline (oracle) ...")
+            out["cpu_baseline"] = cpu_baseline(sd, min(16, os.cpu_count() or 1), args.cpu_rows, args.cpu_frames)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -116,6 +116,12 @@ def load_golden_u8(name: str) -> np.ndarray:
     return np.frombuffer(raw, dtype=np.uint8).reshape(man["height"], man["width"], 3)
 
 
+def ppm_text_from_u8(u8: np.ndarray) -> str:
+    """ASCII P3 text of a u8 image in render_ppm's exact format (render_ppm.rs:51-55)."""
+    h, w, _ = u8.shape
+    return f"P3\n{w} {h} 255\n" + "".join(f"{v} " for v in u8.reshape(-1).tolist())
+
+
 def to_u8(img: np.ndarray) -> np.ndarray:
     """render_ppm's `(v * 255.0) as u8` (render_ppm.rs:48-49): f32 multiply, saturate, truncate, NaN -> 0."""
     v = np.asarray(img, dtype=np.float32) * np.float32(255.0)
