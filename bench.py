@@ -65,16 +65,18 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames-per-launch", type=int, default=32)
+    ap.add_argument("--variant", type=int, default=0, help="sphere-scan kernel (0 default, 1 simple, 2 packed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=24)
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-rows", type=int, default=108)
+    ap.add_argument("--cpu-frames", type=int, default=64)
     args = ap.parse_args()
 
     import numpy as np
     import torch
 
-    import hrt
+    import hrt  # noqa: F401  (loads lib/libhrt.so)
     import scenes
+    from hrt.parallel import gather_image
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -94,7 +96,7 @@ def main() -> int:
     sd = scenes.config_c3(args.width, args.height, args.frames)
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
-    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch)
+    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant)
     local_rows = r.local_rows
     max_rows = (sd.height + world - 1) // world
     part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
@@ -111,14 +113,7 @@ def main() -> int:
         r.draw_frames(sd.frames, 1000, 10)
         r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
         st = r.stats()
-        if dist is not None:
-            dist.gather(part, gathered, dst=0)
-            if rank == 0:
-                for k in range(world):
-                    rows_k = len(range(k, sd.height, world))
-                    full[k::world] = gathered[k][:rows_k]
-        elif rank == 0:
-            full.copy_(part[:local_rows])
+        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full)
         return st
 
     log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
@@ -200,7 +195,7 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": "k_render<sphere>",
+                "kernel": f"k_render<sphere, scan {args.variant or 2}>",
                 "avg_launch_ms": round(avg_launch_ms, 3),
                 "flop_per_launch": flop_per_launch,
                 "alg_hbm_bytes_per_launch": alg_bytes,

@@ -18,7 +18,7 @@
 #include "host/scene.hpp"
 #include "rt_device.hpp"
 
-hipError_t hrt_launch_render(int mode, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 
 namespace {
 
@@ -93,6 +93,7 @@ struct rt_renderer {
     DevBuf<float> image;
     DevBuf<float4> sph_geo;
     DevBuf<hrt_dev::SphereAux> sph_aux;
+    DevBuf<hrt_dev::SpherePair> sph_pairs;
     uint32_t n_spheres = 0;
     DevBuf<float4> nodes;
     DevBuf<hrt_dev::TriDev> tris;
@@ -132,12 +133,29 @@ int upload_spheres(rt_renderer* r) {
                                     s.material.albedo.x, s.material.albedo.y, s.material.albedo.z,
                                     s.material.params.x, s.material.kind, 0, 0, 0};
     }
+    // slot pairs for the packed scan; an odd tail slot is paired with a NaN-centre slot (never accepted)
+    const uint32_t npairs = (nslots + 1) / 2;
+    const float qnan = std::nanf("");
+    std::vector<hrt_dev::SpherePair> pairs(npairs);
+    for (uint32_t p = 0; p < npairs; p++) {
+        for (int k = 0; k < 2; k++) {
+            const uint32_t i = 2 * p + (uint32_t)k;
+            const float4 g = i < nslots ? geo[i] : float4{qnan, qnan, qnan, 0.0f};
+            pairs[p].cx[k] = g.x;
+            pairs[p].cy[k] = g.y;
+            pairs[p].cz[k] = g.z;
+            pairs[p].rr[k] = g.w;
+        }
+    }
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
+    if (!rc) rc = ensure(r->sph_pairs, npairs);
     if (rc) return rc;
     if (nslots) {
         HIP_TRY(hipMemcpyAsync(r->sph_geo.ptr, geo.data(), nslots * sizeof(float4), hipMemcpyHostToDevice, r->stream));
         HIP_TRY(hipMemcpyAsync(r->sph_aux.ptr, aux.data(), nslots * sizeof(aux[0]), hipMemcpyHostToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->sph_pairs.ptr, pairs.data(), npairs * sizeof(pairs[0]), hipMemcpyHostToDevice,
+                               r->stream));
         HIP_TRY(hipStreamSynchronize(r->stream));  // host staging vectors die here
     }
     r->n_spheres = nslots;
@@ -175,6 +193,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.bounces = r->params.bounces;
     P.ema_cap = (float)r->params.ema_cap;
     P.nslots = r->mode == RT_MODE_TRIS ? 0u : r->n_spheres;
+    P.npairs = (P.nslots + 1) / 2;
+    P.sph_pairs = r->sph_pairs.ptr;
     P.n = r->mode == RT_MODE_SPHERE ? 0u : r->bvh_n;
     P.m = r->mode == RT_MODE_SPHERE ? 0u : r->bvh_m;
     P.row0 = r->params.row0;
@@ -195,7 +215,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.nframes = std::min(fpl, count - done);
         P.time0 = time0 + done * dtime;
         P.frame0 = r->frame_count + done;
-        HIP_TRY(hrt_launch_render(r->mode, P, r->stream));
+        HIP_TRY(hrt_launch_render(r->mode, (int)r->params.variant, P, r->stream));
         launches++;
     }
     HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
@@ -274,6 +294,7 @@ int rt_destroy(rt_renderer* r) {
     r->image.release();
     r->sph_geo.release();
     r->sph_aux.release();
+    r->sph_pairs.release();
     r->nodes.release();
     r->tris.release();
     r->mats.release();
@@ -294,6 +315,7 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
+    if (p->variant > 3) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;

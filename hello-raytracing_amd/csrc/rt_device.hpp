@@ -43,6 +43,20 @@ struct MatDev {
 };
 static_assert(sizeof(MatDev) == 32, "MatDev");
 
+// Two sphere slots side by side for the packed-FP32 scan (v_pk_{add,mul,fma}_f32 work on lanes .x/.y):
+// slot 2p in .x, slot 2p+1 in .y. An odd slot count is padded with a NaN-centre slot, which no test
+// can accept (every comparison on NaN is false), so it never changes a result.
+typedef float v2f __attribute__((ext_vector_type(2)));
+struct SpherePair {
+    v2f cx, cy, cz, rr;  // centre and radius*radius
+};
+static_assert(sizeof(SpherePair) == 32, "SpherePair");
+
+// Closest-sphere scan implementations (rt_params.variant).
+constexpr int SCAN_SIMPLE = 1;  // one slot per iteration, exact sqrt/div whenever disc >= 0 && b < 0
+constexpr int SCAN_PACKED = 2;  // slot pairs, packed math, interval filter, exact sqrt/div only on ambiguity
+constexpr int SCAN_DEFER = 3;   // slot pairs, packed math, candidate list in LDS, exact resolution after
+
 // Kernel arguments (passed by value in the kernarg segment).
 struct KParams {
     float eye[4], dir[4], up[4], right[4];
@@ -53,11 +67,13 @@ struct KParams {
     uint32_t bounces;
     float ema_cap;                // f32(SAMPLE_FRAME)
     uint32_t nslots;              // sphere slots scanned (arrayLength semantics)
+    uint32_t npairs;              // ceil(nslots / 2) entries of sph_pairs
     uint32_t n, m;                // bvh_tree_size
     uint32_t row0, row_step, nrows;
     float* image;                 // nrows x W x 3
     const float4* sph_geo;        // (cx, cy, cz, r*r) per slot
     const SphereAux* sph_aux;     // per slot
+    const SpherePair* sph_pairs;  // per slot pair
     const float4* nodes;          // 2 float4 per node: min, max
     const TriDev* tris;
     const MatDev* mats;

@@ -60,6 +60,152 @@ __device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, floa
     return bi;
 }
 
+// The reference's t for slot i, recomputed exactly as the scan computes it (scalar IEEE ops give the
+// same bits as the packed lanes). Returns -1 when the reference would give t = -1 (disc < 0).
+__device__ __forceinline__ float exact_sphere_t(const KParams& P, const Ray& r, int i, float a4, float a2) {
+    const float4 g = P.sph_geo[i];
+    const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
+    const float bd = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+    const float b = bd + bd;
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
+    const float disc = __builtin_fmaf(b, b, (-a4) * c);
+    if (disc < 0.0f) return -1.0f;
+    return (-b - __builtin_sqrtf(disc)) / a2;
+}
+
+// Packed scan, bit-identical to scan_spheres. Two slots per iteration with v_pk_* math. A candidate
+// (disc >= 0, b <= 0) first gets an interval [ta - m, ta + m] from the hardware approximate sqrt and
+// reciprocal that provably contains the reference's correctly rounded t (error <= ~2^-19 (|b|+s)/(2a),
+// m = 2^-16 (|b|+s)/(2a) + 2^-60/(2a)); the correctly rounded sqrt/div run only when the interval cannot
+// decide the reference comparison (t > 0 && t < best, first slot wins ties). NaN/inf in the
+// approximation always falls through to the exact path.
+__device__ __forceinline__ int scan_spheres_packed(const KParams& P, const Ray& r, float& best) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    // The interval bound assumes a normal, non-huge 2a (v_rcp_f32 flushes outside that range).
+    if (!(a2 > 0x1p-100f && a2 < 0x1p100f)) return scan_spheres(P, r, best);
+    const float ra2 = __builtin_amdgcn_rcpf(a2);
+    const float mr = ra2 * 0x1p-16f, mc = ra2 * 0x1p-60f;
+    const v2f ox = {r.o.x, r.o.x}, oy = {r.o.y, r.o.y}, oz = {r.o.z, r.o.z};
+    const v2f dx = {r.d.x, r.d.x}, dy = {r.d.y, r.d.y}, dz = {r.d.z, r.d.z};
+    const v2f na4 = {-a4, -a4};
+    float lo_best = best, hi_best = best;  // bounds on the exact t of the current winner
+    bool exact_best = true;
+    int bi = -1;
+
+    auto candidate = [&](int i, float disc, float b) {
+        const float nb = -b;
+        const float s1 = __builtin_amdgcn_sqrtf(disc);
+        const float ta = (nb - s1) * ra2;
+        const float m = __builtin_fmaf(nb + s1, mr, mc);
+        const float lo = ta - m, hi = ta + m;
+        if (hi <= 0.0f) return;                      // t <= 0: rejected
+        if (lo > 0.0f && hi < lo_best) {             // certainly 0 < t < best
+            lo_best = lo; hi_best = hi; bi = i; exact_best = false;
+            return;
+        }
+        if (lo > 0.0f && lo >= hi_best) return;      // certainly t >= best (ties keep the earlier slot)
+        // ambiguous: decide with the reference's exact arithmetic
+        if (!exact_best) {
+            const float tb = exact_sphere_t(P, r, bi, a4, a2);
+            lo_best = hi_best = tb;
+            exact_best = true;
+        }
+        const float t = (nb - __builtin_sqrtf(disc)) / a2;
+        if (t > 0.0f && t < lo_best) {
+            lo_best = hi_best = t;
+            bi = i;
+        }
+    };
+
+    const SpherePair* __restrict__ pairs = P.sph_pairs;
+    const uint32_t np = P.npairs;
+#pragma unroll 2
+    for (uint32_t p = 0; p < np; p++) {
+        const SpherePair q = pairs[p];  // wave-uniform: scalar loads
+        const v2f ocx = ox - q.cx, ocy = oy - q.cy, ocz = oz - q.cz;
+        v2f bd = ocx * dx;
+        bd = __builtin_elementwise_fma(ocy, dy, bd);
+        bd = __builtin_elementwise_fma(ocz, dz, bd);
+        const v2f b = bd + bd;
+        v2f cd = ocx * ocx;
+        cd = __builtin_elementwise_fma(ocy, ocy, cd);
+        cd = __builtin_elementwise_fma(ocz, ocz, cd);
+        const v2f c = cd - q.rr;
+        const v2f disc = __builtin_elementwise_fma(b, b, na4 * c);
+        const float x0 = __builtin_fminf(disc.x, -b.x);
+        const float x1 = __builtin_fminf(disc.y, -b.y);
+        if (__builtin_fmaxf(x0, x1) >= 0.0f) {
+            if (x0 >= 0.0f) candidate((int)(2 * p), disc.x, b.x);
+            if (x1 >= 0.0f) candidate((int)(2 * p + 1), disc.y, b.y);
+        }
+    }
+    if (bi >= 0 && !exact_best) lo_best = exact_sphere_t(P, r, bi, a4, a2);
+    best = lo_best;
+    return bi;
+}
+
+// Deferred scan, bit-identical to scan_spheres. Pass 1 (uniform over all slot pairs, packed math)
+// only decides which pairs hold a candidate (disc >= 0 && b <= 0, or NaN: conservative) and appends
+// the pair index to this lane's list in LDS (ascending). Pass 2 resolves the few candidates with the
+// reference's exact arithmetic in slot order, so `t > 0 && t < best` and first-slot-wins ties are
+// reproduced literally. A lane whose list overflows falls back to the full exact scan.
+constexpr int CAND_CAP = 15;  // list entries per lane; slot CAND_CAP is a write sink past overflow
+
+__device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray& r, float& best,
+                                                     uint16_t* __restrict__ lds_list) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    const v2f ox = {r.o.x, r.o.x}, oy = {r.o.y, r.o.y}, oz = {r.o.z, r.o.z};
+    const v2f dx = {r.d.x, r.d.x}, dy = {r.d.y, r.d.y}, dz = {r.d.z, r.d.z};
+    const v2f na4 = {-a4, -a4};
+    uint32_t cnt = 0;
+
+    const SpherePair* __restrict__ pairs = P.sph_pairs;
+    const uint32_t np = P.npairs;
+#pragma unroll 2
+    for (uint32_t p = 0; p < np; p++) {
+        const SpherePair q = pairs[p];  // wave-uniform: scalar loads
+        const v2f ocx = ox - q.cx, ocy = oy - q.cy, ocz = oz - q.cz;
+        v2f bd = ocx * dx;
+        bd = __builtin_elementwise_fma(ocy, dy, bd);
+        bd = __builtin_elementwise_fma(ocz, dz, bd);
+        const v2f b = bd + bd;
+        v2f cd = ocx * ocx;
+        cd = __builtin_elementwise_fma(ocy, ocy, cd);
+        cd = __builtin_elementwise_fma(ocz, ocz, cd);
+        const v2f c = cd - q.rr;
+        const v2f disc = __builtin_elementwise_fma(b, b, na4 * c);
+        const float x0 = __builtin_fminf(disc.x, -b.x);
+        const float x1 = __builtin_fminf(disc.y, -b.y);
+        if (__builtin_fmaxf(x0, x1) >= 0.0f) {
+            lds_list[(cnt < (uint32_t)CAND_CAP ? cnt : (uint32_t)CAND_CAP) * 256u] = (uint16_t)p;
+            cnt++;
+        }
+    }
+    if (cnt > (uint32_t)CAND_CAP) return scan_spheres(P, r, best);  // overflow: exact full scan
+
+    int bi = -1;
+    float bt = best;
+    for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t p = lds_list[k * 256u];
+#pragma unroll
+        for (uint32_t s = 0; s < 2; s++) {
+            const uint32_t i = 2 * p + s;
+            if (i >= P.nslots) break;
+            const float t = exact_sphere_t(P, r, (int)i, a4, a2);
+            if (t > 0.0f && t < bt) {
+                bt = t;
+                bi = (int)i;
+            }
+        }
+    }
+    best = bt;
+    return bi;
+}
+
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
     const f3 p = point_on_ray(r.o, r.d, t);
@@ -133,12 +279,14 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h)
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h) {
+template <int MODE, int SCAN>
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, uint16_t* lds_list) {
     h.t = FLT_MAX_REF;
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
-        const int bi = scan_spheres(P, r, best);
+        const int bi = SCAN == SCAN_DEFER    ? scan_spheres_deferred(P, r, best, lds_list)
+                       : SCAN == SCAN_PACKED ? scan_spheres_packed(P, r, best)
+                                             : scan_spheres(P, r, best);
         if (bi >= 0) sphere_record(P, r, bi, best, h);
     }
     if (MODE != MODE_SPHERE) walk_bvh(P, r, h);
@@ -231,9 +379,14 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 }  // namespace
 
 // One launch = P.nframes frames over this renderer's rows. Grid: (ceil(W/16), ceil(nrows/16)).
-template <int MODE>
+template <int MODE, int SCAN>
 __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint16_t* lds_list = nullptr;
+    if constexpr (SCAN == SCAN_DEFER) {
+        __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
+        lds_list = cand + threadIdx.x;
+    }
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool valid = x < P.W && kr < P.nrows;
@@ -263,7 +416,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE>(P, ray, h);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list);
             queries++;
             if (hit) {
                 scatter<MODE>(s, ray, h);
@@ -305,19 +458,24 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     if (lane == 0 && qsum) atomicAdd(P.counter, qsum);
 }
 
-template __global__ void k_render<MODE_SPHERE>(const KParams);
-template __global__ void k_render<MODE_TRIS>(const KParams);
-template __global__ void k_render<MODE_MIXED>(const KParams);
-
-// Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI).
-hipError_t hrt_launch_render(int mode, const KParams& P, hipStream_t stream) {
+// Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI). variant: SCAN_* (0 = default).
+hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((P.W + 15u) / 16u, (P.nrows + 15u) / 16u);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    if (variant == 0) variant = SCAN_DEFER;
     switch (mode) {
-    case MODE_SPHERE: hipLaunchKernelGGL(k_render<MODE_SPHERE>, grid, block, 0, stream, P); break;
-    case MODE_TRIS: hipLaunchKernelGGL(k_render<MODE_TRIS>, grid, block, 0, stream, P); break;
-    default: hipLaunchKernelGGL(k_render<MODE_MIXED>, grid, block, 0, stream, P); break;
+    case MODE_SPHERE:
+        if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_SIMPLE>), grid, block, 0, stream, P);
+        else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_PACKED>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
+        break;
+    case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
+    default:
+        if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_SIMPLE>), grid, block, 0, stream, P);
+        else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_PACKED>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
+        break;
     }
     return hipGetLastError();
 }

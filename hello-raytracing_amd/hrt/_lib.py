@@ -34,6 +34,7 @@ class RtParams(C.Structure):
         ("row0", C.c_uint32),
         ("row_step", C.c_uint32),
         ("frames_per_launch", C.c_uint32),
+        ("variant", C.c_uint32),
     ]
 
 

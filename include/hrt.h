@@ -60,6 +60,8 @@ typedef struct rt_params {
     uint32_t min_sphere_slots; /* arrayLength(&scene) floor; default 100 (zero-filled slots traced)    */
     uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
+    uint32_t variant;          /* sphere-scan kernel: 0 default (= 3), 1 simple, 2 packed + interval filter,
+                                  3 packed + deferred exact candidates; all bit-identical   */
 } rt_params;
 
 typedef struct rt_stats {

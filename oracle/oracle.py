@@ -92,6 +92,8 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
         image = np.ascontiguousarray(image, dtype=np.float32).copy()
         assert image.shape == (nrows, nx, 3)
     cam = np.ascontiguousarray(camera).tobytes()
+    if threads <= 0:  # explicit: importing torch can leave the OpenMP default at one thread
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     q = lib().oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
                             image.ctypes.data, threads)
     return image, int(q)

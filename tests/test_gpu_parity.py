@@ -154,6 +154,34 @@ def test_rtiow_cover_scene_small():
     assert r.stats().queries == q
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_scan_variants_bit_identical(variant):
+    """Every sphere-scan kernel variant gives the same bits (and ray counts) as the oracle."""
+    for sd in (scenes.config_c3(192, 108, 4), scenes.golden_scene("dielectric_materials", 128, 128),
+               scenes.golden_scene("complex_scene", 128, 128)):
+        sd.frames = 4
+        r = scenes.make_renderer(sd)
+        r.set_params(variant=variant)
+        r.draw_frames(sd.frames, 1000, 10)
+        ref, q = scenes.oracle_render(sd)
+        assert_parity(r.read_image(), ref, f"{sd.name} variant {variant}")
+        assert r.stats().queries == q
+
+
+def test_scan_variants_agree_at_scale():
+    """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
+    sd = scenes.config_c3(640, 360, 32)
+    imgs = []
+    for variant in (1, 2, 3):
+        r = scenes.make_renderer(sd)
+        r.set_params(variant=variant)
+        r.draw_frames(sd.frames, 1000, 10)
+        imgs.append((r.read_image(), r.stats().queries))
+    for img, q in imgs[1:]:
+        np.testing.assert_array_equal(imgs[0][0].view(np.uint32), img.view(np.uint32))
+        assert imgs[0][1] == q
+
+
 def test_suzanne_tris_mode_vs_oracle():
     scene = hrt.SceneTris.new_suzane(128, 96)
     scene.init()
