@@ -31,6 +31,7 @@ for p in (ROOT, ROOT / "hello-raytracing_amd", ROOT / "tests"):
 FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak with packed FMA (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 SPHERE_TEST_FLOP = 18  # per ray-sphere test (a, 4a hoisted per query)
+BOX_TEST_FLOP = 12  # per padded slab test: 6 adds + 6 multiplies
 
 
 def log(msg: str) -> None:
@@ -65,7 +66,8 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames-per-launch", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=0, help="sphere-scan kernel (0 default, 1 simple, 2 packed)")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=64)
@@ -129,16 +131,24 @@ def main() -> int:
     queries = 0
     kernel_ms = 0.0
     launches = 0
+    box_tests = 0
+    sphere_tests = 0
+    variant = 0
     for i in range(args.steps):
         st = step()
         queries += st.queries
         kernel_ms += st.kernel_ms
         launches += st.launches
-        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernel {st.kernel_ms:.1f} ms")
+        box_tests += st.box_tests
+        sphere_tests += st.sphere_tests
+        variant = st.variant
+        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernel {st.kernel_ms:.1f} ms, "
+            f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
     barrier()
     elapsed = time.perf_counter() - t0
 
-    stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches)], dtype=torch.float64, device=dev)
+    stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches), float(box_tests),
+                            float(sphere_tests)], dtype=torch.float64, device=dev)
     if dist is not None:
         all_t = [torch.zeros_like(stats_t) for _ in range(world)]
         dist.all_gather(all_t, stats_t)
@@ -150,11 +160,17 @@ def main() -> int:
 
     if rank == 0:
         value = total_q / t_max / 1e6
-        # roofline of the render kernel on rank 0: algorithmic FLOPs per launch / HIP-event launch time
+        # roofline of the render kernel on rank 0: algorithmic FLOPs per launch / HIP-event launch time.
+        # FLOPs are the tests the kernel actually ran (exact counters): 18 per ray-sphere test (SURVEY
+        # 8(d)), 12 per padded box test (6 sub + 6 mul); brute_force_equiv prices the reference algorithm
+        # (every slot for every ray) at the same time.
         my_q, my_ms, my_launches = float(all_t[0, 1]), float(all_t[0, 2]), float(all_t[0, 3])
-        avg_launch_ms = my_ms / max(my_launches, 1.0)
-        flop_per_launch = SPHERE_TEST_FLOP * nslots * my_q / max(my_launches, 1.0)
+        my_box, my_sph = float(all_t[0, 4]), float(all_t[0, 5])
+        nl = max(my_launches, 1.0)
+        avg_launch_ms = my_ms / nl
+        flop_per_launch = (SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box) / nl
         achieved = flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
+        brute_equiv = SPHERE_TEST_FLOP * nslots * my_q / nl / (avg_launch_ms * 1e-3) / 1e12
         px = local_rows * sd.width
         alg_bytes = 24.0 * px + 64.0 * nslots  # framebuffer read+write per launch + sphere arrays
         traffic = None
@@ -195,7 +211,10 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": f"k_render<sphere, scan {args.variant or 2}>",
+                "kernel": f"k_render<sphere, scan variant {variant}>",
+                "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),
+                "box_tests_per_ray": round(my_box / max(my_q, 1.0), 3),
+                "brute_force_equiv_tflops": round(brute_equiv, 3),
                 "avg_launch_ms": round(avg_launch_ms, 3),
                 "flop_per_launch": flop_per_launch,
                 "alg_hbm_bytes_per_launch": alg_bytes,

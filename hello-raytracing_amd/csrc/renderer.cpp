@@ -16,6 +16,7 @@
 
 #include "../../include/hrt.h"
 #include "host/scene.hpp"
+#include "host/sphere_bvh.hpp"
 #include "rt_device.hpp"
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
@@ -95,6 +96,10 @@ struct rt_renderer {
     DevBuf<hrt_dev::SphereAux> sph_aux;
     DevBuf<hrt_dev::SpherePair> sph_pairs;
     uint32_t n_spheres = 0;
+    // culling BVH over the sphere slots (SCAN_BVH)
+    DevBuf<float4> bvh_nodes, bvh_sph;
+    DevBuf<int> bvh_slot, bvh_large;
+    hrt::SphereBvh bvh_host;
     DevBuf<float4> nodes;
     DevBuf<hrt_dev::TriDev> tris;
     DevBuf<hrt_dev::MatDev> mats;
@@ -106,6 +111,7 @@ struct rt_renderer {
 
     rt_stats stats{};
     bool timing_pending = false;
+    int last_variant = 0;
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
@@ -147,19 +153,63 @@ int upload_spheres(rt_renderer* r) {
             pairs[p].rr[k] = g.w;
         }
     }
+    // culling BVH: boxes stored relative to the root centre (rounded outward again after the shift)
+    std::vector<float> cr(4 * (size_t)nslots);
+    for (uint32_t i = 0; i < nslots; i++) {
+        const bool real = i < r->spheres.size();
+        cr[4 * i + 0] = geo[i].x;
+        cr[4 * i + 1] = geo[i].y;
+        cr[4 * i + 2] = geo[i].z;
+        cr[4 * i + 3] = real ? r->spheres[i].radius : 0.0f;
+    }
+    r->bvh_host = hrt::build_sphere_bvh(cr);
+    const hrt::SphereBvh& B = r->bvh_host;
+    std::vector<float4> bnodes(4 * std::max<size_t>(B.nodes.size(), 1));
+    auto rel_lo = [&](float v, int k) { return std::nextafter((float)((double)v - (double)B.root_center[k]), -INFINITY); };
+    auto rel_hi = [&](float v, int k) { return std::nextafter((float)((double)v - (double)B.root_center[k]), INFINITY); };
+    for (size_t j = 0; j < B.nodes.size(); j++) {
+        const hrt::SphereBvhNode& n = B.nodes[j];
+        float4* o = &bnodes[4 * j];
+        o[0] = float4{rel_lo(n.lmin[0], 0), rel_lo(n.lmin[1], 1), rel_lo(n.lmin[2], 2), __builtin_bit_cast(float, n.left)};
+        o[1] = float4{rel_hi(n.lmax[0], 0), rel_hi(n.lmax[1], 1), rel_hi(n.lmax[2], 2), 0.0f};
+        o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
+        o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
+    }
+    const size_t nleaf = B.slot.size();
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
     if (!rc) rc = ensure(r->sph_pairs, npairs);
+    if (!rc) rc = ensure(r->bvh_nodes, bnodes.size());
+    if (!rc) rc = ensure(r->bvh_sph, std::max<size_t>(nleaf, 1));
+    if (!rc) rc = ensure(r->bvh_slot, std::max<size_t>(nleaf, 1));
+    if (!rc) rc = ensure(r->bvh_large, std::max<size_t>(B.large.size(), 1));
     if (rc) return rc;
     if (nslots) {
         HIP_TRY(hipMemcpyAsync(r->sph_geo.ptr, geo.data(), nslots * sizeof(float4), hipMemcpyHostToDevice, r->stream));
         HIP_TRY(hipMemcpyAsync(r->sph_aux.ptr, aux.data(), nslots * sizeof(aux[0]), hipMemcpyHostToDevice, r->stream));
         HIP_TRY(hipMemcpyAsync(r->sph_pairs.ptr, pairs.data(), npairs * sizeof(pairs[0]), hipMemcpyHostToDevice,
                                r->stream));
+        HIP_TRY(hipMemcpyAsync(r->bvh_nodes.ptr, bnodes.data(), bnodes.size() * sizeof(float4),
+                               hipMemcpyHostToDevice, r->stream));
+        if (nleaf) {
+            HIP_TRY(hipMemcpyAsync(r->bvh_sph.ptr, B.sph.data(), nleaf * sizeof(float4), hipMemcpyHostToDevice,
+                                   r->stream));
+            HIP_TRY(hipMemcpyAsync(r->bvh_slot.ptr, B.slot.data(), nleaf * sizeof(int), hipMemcpyHostToDevice,
+                                   r->stream));
+        }
+        if (!B.large.empty())
+            HIP_TRY(hipMemcpyAsync(r->bvh_large.ptr, B.large.data(), B.large.size() * sizeof(int),
+                                   hipMemcpyHostToDevice, r->stream));
         HIP_TRY(hipStreamSynchronize(r->stream));  // host staging vectors die here
     }
     r->n_spheres = nslots;
     return RT_OK;
+}
+
+// variant 0 = the fastest exact scan for the scene: the culling BVH from 32 slots up, else the deferred scan.
+int resolve_variant(const rt_renderer* r) {
+    if (r->params.variant) return (int)r->params.variant;
+    return r->n_spheres >= 32 ? hrt_dev::SCAN_BVH : hrt_dev::SCAN_DEFER;
 }
 
 int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime) {
@@ -168,9 +218,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         int rc = upload_spheres(r);  // empty scene: min_sphere_slots zero slots, like an unwritten buffer
         if (rc) return rc;
     }
-    int rc = ensure(r->counter, 1);
+    int rc = ensure(r->counter, 4);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, sizeof(unsigned long long), r->stream));
+    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, 4 * sizeof(unsigned long long), r->stream));
 
     hrt_dev::KParams P{};
     const hrt::Camera& c = r->camera;
@@ -207,6 +257,23 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.tris = r->tris.ptr;
     P.mats = r->mats.ptr;
     P.counter = r->counter.ptr;
+    const hrt::SphereBvh& B = r->bvh_host;
+    P.bvh_nodes = r->bvh_nodes.ptr;
+    P.bvh_sph = r->bvh_sph.ptr;
+    P.bvh_slot = r->bvh_slot.ptr;
+    P.large_slots = r->bvh_large.ptr;
+    P.nlarge = (uint32_t)B.large.size();
+    P.bvh_root = B.root_word;
+    for (int k = 0; k < 3; k++) P.bvh_rc[k] = B.root_center[k];
+    P.bvh_rr = B.root_radius;
+    // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
+    const float u = 0x1p-24f;
+    P.pad_k1 = 8.0f * u * B.r_max;
+    P.pad_k2 = B.r_min > 0.0f ? 16.0f * u / B.r_min : INFINITY;
+    P.pad_k3 = 2e-3f;
+    P.pad_k4 = 4.0f * u;
+    const int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
+    r->last_variant = variant;
 
     const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
     HIP_TRY(hipEventRecord(r->ev_start, r->stream));
@@ -215,7 +282,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.nframes = std::min(fpl, count - done);
         P.time0 = time0 + done * dtime;
         P.frame0 = r->frame_count + done;
-        HIP_TRY(hrt_launch_render(r->mode, (int)r->params.variant, P, r->stream));
+        HIP_TRY(hrt_launch_render(r->mode, variant, P, r->stream));
         launches++;
     }
     HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
@@ -233,10 +300,13 @@ int finish_stats(rt_renderer* r) {
     HIP_TRY(hipEventSynchronize(r->ev_stop));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
-    unsigned long long q = 0;
-    HIP_TRY(hipMemcpy(&q, r->counter.ptr, sizeof(q), hipMemcpyDeviceToHost));
+    unsigned long long q[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpy(q, r->counter.ptr, sizeof(q), hipMemcpyDeviceToHost));
     r->stats.kernel_ms = ms;
-    r->stats.queries = q;
+    r->stats.queries = q[0];
+    r->stats.box_tests = q[1];
+    r->stats.sphere_tests = q[2];
+    r->stats.variant = (uint32_t)r->last_variant;
     r->timing_pending = false;
     return RT_OK;
 }
@@ -315,7 +385,7 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
-    if (p->variant > 3) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->variant > 4) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;

@@ -56,6 +56,9 @@ static_assert(sizeof(SpherePair) == 32, "SpherePair");
 constexpr int SCAN_SIMPLE = 1;  // one slot per iteration, exact sqrt/div whenever disc >= 0 && b < 0
 constexpr int SCAN_PACKED = 2;  // slot pairs, packed math, interval filter, exact sqrt/div only on ambiguity
 constexpr int SCAN_DEFER = 3;   // slot pairs, packed math, candidate list in LDS, exact resolution after
+constexpr int SCAN_BVH = 4;     // conservative BVH culling + exact tests, (t, slot) lexicographic min
+constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
+constexpr int BVH_STACK = 24;   // traversal stack entries per lane (LDS); overflow -> exact full scan
 
 // Kernel arguments (passed by value in the kernarg segment).
 struct KParams {
@@ -74,10 +77,18 @@ struct KParams {
     const float4* sph_geo;        // (cx, cy, cz, r*r) per slot
     const SphereAux* sph_aux;     // per slot
     const SpherePair* sph_pairs;  // per slot pair
+    // SCAN_BVH culling structure (host/sphere_bvh.hpp); boxes are relative to bvh_rc
+    const float4* bvh_nodes;      // 4 float4 per node: lmin|left, lmax, rmin|right, rmax
+    const float4* bvh_sph;        // leaf spheres in BVH order: cx, cy, cz, r*r
+    const int* bvh_slot;          // original slot of each leaf sphere
+    const int* large_slots;       // slots scanned linearly for every ray
+    uint32_t nlarge, bvh_root;    // large-list length, root child word
+    float bvh_rc[3], bvh_rr;      // root box centre and radius bound
+    float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     const float4* nodes;          // 2 float4 per node: min, max
     const TriDev* tris;
     const MatDev* mats;
-    unsigned long long* counter;  // closest-hit queries
+    unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
 };
 
 struct f3 {

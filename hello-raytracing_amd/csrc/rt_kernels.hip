@@ -206,6 +206,123 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
     return bi;
 }
 
+struct Tally {
+    uint32_t boxes = 0, spheres = 0;
+};
+
+// (t, slot) lexicographic minimum = the reference's linear scan: strict `t < best` keeps the first slot
+// among equal t, so a later-visited lower slot with the same t must win.
+__device__ __forceinline__ bool beats(float t, int i, float bt, int bi) {
+    return t > 0.0f && (t < bt || (t == bt && bi >= 0 && i < bi));
+}
+
+// The reference's t for a sphere given its (cx, cy, cz, r*r) — same ops as exact_sphere_t.
+__device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float a4, float a2) {
+    const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
+    const float bd = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+    const float b = bd + bd;
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
+    const float disc = __builtin_fmaf(b, b, (-a4) * c);
+    if (!(disc >= 0.0f && b <= 0.0f)) return -1.0f;  // t would be <= 0, NaN or -1: never accepted
+    return (-b - __builtin_sqrtf(disc)) / a2;
+}
+
+__device__ __forceinline__ float robust_inv(float d) {
+    return __builtin_fabsf(d) >= 1e-30f ? 1.0f / d : __builtin_copysignf(1e30f, d);
+}
+
+// Slab test of the ray against a box padded by `pad` on every side (box relative to bvh_rc; lo/hi already
+// hold -o' -/+ pad). Visits when the padded box is entered before it is left, not behind the origin,
+// and not beyond the current best t (equality visits: ties must be seen).
+__device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx, const f3& lo, const f3& hi,
+                                               const f3& inv, float bt, float& tenter) {
+    const float t0x = (mn.x + lo.x) * inv.x, t1x = (mx.x + hi.x) * inv.x;
+    const float t0y = (mn.y + lo.y) * inv.y, t1y = (mx.y + hi.y) * inv.y;
+    const float t0z = (mn.z + lo.z) * inv.z, t1z = (mx.z + hi.z) * inv.z;
+    const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmax_ieee(fmin_ieee(t0z, t1z), 0.0f));
+    const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmin_ieee(fmax_ieee(t0z, t1z), bt));
+    tenter = tmin;
+    return tmin <= tmax;
+}
+
+// BVH scan, bit-identical to scan_spheres: every sphere the reference could accept lies in a box the
+// padded slab test visits (float-error bound on the discriminant, DESIGN.md §Sphere BVH exactness), every
+// visited sphere is tested with the reference arithmetic, and the winner is the (t, slot) minimum.
+// Rays the bound does not cover (non-finite origin, 2a outside [2^-100, 2^100]) or a stack overflow fall
+// back to the full exact scan.
+__device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
+                                                Tally& tally) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
+    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    float bt = best;
+    int bi = -1;
+    for (uint32_t k = 0; k < P.nlarge; k++) {
+        const int i = P.large_slots[k];
+        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
+        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+    }
+    tally.spheres += P.nlarge;
+
+    // per-query padding: delta >= the distance by which a float-accepted sphere can miss geometrically
+    const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
+    const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
+    const float D = dl * 1.001f + P.bvh_rr;
+    const float dn = __builtin_amdgcn_sqrtf(a);
+    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
+    const float pad = 2.02f * delta;
+    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+
+    uint32_t node = P.bvh_root;
+    int sp = 0;
+    bool overflow = false;
+    while (true) {
+        if (!(node & BVH_LEAF_BIT)) {
+            const float4 n0 = P.bvh_nodes[4 * node + 0];
+            const float4 n1 = P.bvh_nodes[4 * node + 1];
+            const float4 n2 = P.bvh_nodes[4 * node + 2];
+            const float4 n3 = P.bvh_nodes[4 * node + 3];
+            float tl, tr;
+            const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
+            const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
+            tally.boxes += 2;
+            const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
+            if (hl && hr) {
+                const bool lfirst = tl <= tr;
+                if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
+                else overflow = true;
+                node = lfirst ? left : right;
+                continue;
+            }
+            if (hl) { node = left; continue; }
+            if (hr) { node = right; continue; }
+        } else {
+            const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+            for (uint32_t j = 0; j < cnt; j++) {
+                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
+                const int i = P.bvh_slot[first + j];
+                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+            }
+            tally.spheres += cnt;
+        }
+        if (sp == 0) break;
+        node = stack[(--sp) * 256];
+    }
+    if (overflow) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    best = bt;
+    return bi;
+}
+
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
     const f3 p = point_on_ray(r.o, r.d, t);
@@ -280,13 +397,23 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h)
 }
 
 template <int MODE, int SCAN>
-__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, uint16_t* lds_list) {
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally) {
     h.t = FLT_MAX_REF;
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
-        const int bi = SCAN == SCAN_DEFER    ? scan_spheres_deferred(P, r, best, lds_list)
-                       : SCAN == SCAN_PACKED ? scan_spheres_packed(P, r, best)
-                                             : scan_spheres(P, r, best);
+        int bi;
+        if constexpr (SCAN == SCAN_BVH) {
+            bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
+        } else if constexpr (SCAN == SCAN_DEFER) {
+            bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
+            tally.spheres += P.nslots;
+        } else if constexpr (SCAN == SCAN_PACKED) {
+            bi = scan_spheres_packed(P, r, best);
+            tally.spheres += P.nslots;
+        } else {
+            bi = scan_spheres(P, r, best);
+            tally.spheres += P.nslots;
+        }
         if (bi >= 0) sphere_record(P, r, bi, best, h);
     }
     if (MODE != MODE_SPHERE) walk_bvh(P, r, h);
@@ -382,11 +509,15 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 template <int MODE, int SCAN>
 __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint16_t* lds_list = nullptr;
+    void* lds_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
+    } else if constexpr (SCAN == SCAN_BVH) {
+        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+        lds_list = bvh_stack + threadIdx.x;
     }
+    Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool valid = x < P.W && kr < P.nrows;
@@ -416,7 +547,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
             queries++;
             if (hit) {
                 scatter<MODE>(s, ray, h);
@@ -451,11 +582,19 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         px[1] = acc1;
         px[2] = acc2;
     }
-    // One atomic per wave for the ray count.
-    unsigned long long qsum = queries;
+    // One atomic per wave and counter: rays, box tests, exact sphere tests.
+    unsigned long long qsum = queries, bsum = tally.boxes, ssum = tally.spheres;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) qsum += __shfl_xor(qsum, off);
-    if (lane == 0 && qsum) atomicAdd(P.counter, qsum);
+    for (int off = 32; off > 0; off >>= 1) {
+        qsum += __shfl_xor(qsum, off);
+        bsum += __shfl_xor(bsum, off);
+        ssum += __shfl_xor(ssum, off);
+    }
+    if (lane == 0) {
+        if (qsum) atomicAdd(P.counter, qsum);
+        if (bsum) atomicAdd(P.counter + 1, bsum);
+        if (ssum) atomicAdd(P.counter + 2, ssum);
+    }
 }
 
 // Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI). variant: SCAN_* (0 = default).
@@ -463,17 +602,19 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
     dim3 block(256);
     dim3 grid((P.W + 15u) / 16u, (P.nrows + 15u) / 16u);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    if (variant == 0) variant = SCAN_DEFER;
+    // variant 0 is resolved by the host (renderer.cpp) before the launch
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_SIMPLE>), grid, block, 0, stream, P);
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_PACKED>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
     default:
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_SIMPLE>), grid, block, 0, stream, P);
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_PACKED>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     }

@@ -45,6 +45,10 @@ class RtStats(C.Structure):
         ("kernel_ms", C.c_double),
         ("launches", C.c_uint32),
         ("local_rows", C.c_uint32),
+        ("box_tests", C.c_uint64),
+        ("sphere_tests", C.c_uint64),
+        ("variant", C.c_uint32),
+        ("pad0", C.c_uint32),
     ]
 
 

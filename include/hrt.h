@@ -60,8 +60,9 @@ typedef struct rt_params {
     uint32_t min_sphere_slots; /* arrayLength(&scene) floor; default 100 (zero-filled slots traced)    */
     uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
-    uint32_t variant;          /* sphere-scan kernel: 0 default (= 3), 1 simple, 2 packed + interval filter,
-                                  3 packed + deferred exact candidates; all bit-identical   */
+    uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots up, else 3), 1 simple,
+                                  2 packed + interval filter, 3 packed + deferred exact candidates,
+                                  4 conservative culling BVH; all bit-identical   */
 } rt_params;
 
 typedef struct rt_stats {
@@ -70,6 +71,10 @@ typedef struct rt_stats {
     double kernel_ms;      /* HIP-event time of the last draw call's kernels, on the renderer stream   */
     uint32_t launches;     /* kernel launches of the last draw call                                    */
     uint32_t local_rows;   /* rows owned by this renderer                                              */
+    uint64_t box_tests;    /* padded-box tests of the sphere culling BVH (variant 4), last draw call    */
+    uint64_t sphere_tests; /* ray-sphere tests (slots scanned, or BVH leaf + large-list tests)          */
+    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..4)                         */
+    uint32_t pad0;
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

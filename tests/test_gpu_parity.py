@@ -154,7 +154,7 @@ def test_rtiow_cover_scene_small():
     assert r.stats().queries == q
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_scan_variants_bit_identical(variant):
     """Every sphere-scan kernel variant gives the same bits (and ray counts) as the oracle."""
     for sd in (scenes.config_c3(192, 108, 4), scenes.golden_scene("dielectric_materials", 128, 128),
@@ -172,7 +172,7 @@ def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
     imgs = []
-    for variant in (1, 2, 3):
+    for variant in (1, 2, 3, 4):
         r = scenes.make_renderer(sd)
         r.set_params(variant=variant)
         r.draw_frames(sd.frames, 1000, 10)
@@ -180,6 +180,65 @@ def test_scan_variants_agree_at_scale():
     for img, q in imgs[1:]:
         np.testing.assert_array_equal(imgs[0][0].view(np.uint32), img.view(np.uint32))
         assert imgs[0][1] == q
+
+
+def _random_scene(kind: str, seed: int):
+    """Adversarial sphere sets for the culling BVH (>= 32 slots): tangent grids, radius spread over
+    three decades, far-from-origin coordinates, zero-radius slots, every material."""
+    rng = np.random.default_rng(seed)
+    o = []
+    mats = [lambda c, r: hrt.Sphere.new_lambertian(c, r, hrt.Vec3(*rng.uniform(0.1, 0.9, 3))),
+            lambda c, r: hrt.Sphere.new_metal(c, r, hrt.Vec3(*rng.uniform(0.3, 0.9, 3)), float(rng.uniform(0, 0.5))),
+            lambda c, r: hrt.Sphere.new_dielectric(c, r, float(rng.choice([1.33, 1.5, 2.4])))]
+    off = np.zeros(3)
+    if kind == "tangent_grid":  # spheres touching their neighbours: ties and grazing rays
+        for i in range(-4, 4):
+            for j in range(-4, 4):
+                o.append(mats[(i + j) % 3](hrt.Vec3(float(i), 0.5, float(j) - 5.0), 0.5))
+    elif kind == "radius_spread":
+        for _ in range(120):
+            c = rng.uniform([-4, -1, -9], [4, 3, -2])
+            o.append(mats[rng.integers(3)](hrt.Vec3(*c), float(10 ** rng.uniform(-3, 0))))
+    elif kind == "far_offset":  # the whole scene (and camera) 1e4 units away from the origin
+        off = np.array([1.0e4, -2.0e4, 3.0e4])
+        for _ in range(64):
+            c = rng.uniform([-3, -1, -8], [3, 2, -3]) + off
+            o.append(mats[rng.integers(3)](hrt.Vec3(*c), float(rng.uniform(0.1, 0.6))))
+    o.append(hrt.Sphere.new_lambertian(hrt.Vec3(*(np.array([0.0, -1000.5, -5.0]) + off)), 1000.0,
+                                       hrt.Vec3(0.5, 0.5, 0.5)))
+    cam = hrt.Camera.new(hrt.Vec3(*(np.array([0.5, 2.0, 3.0]) + off)), hrt.Vec3(*(np.array([0.0, 0.0, -5.0]) + off)),
+                         6.0, 0.1, 0.9)
+    return scenes.SceneDef(kind, hrt.RT_MODE_SPHERE, 96, 64, cam, hrt.spheres_array(o), frames=6, bounces=50,
+                           min_sphere_slots=0)
+
+
+@pytest.mark.parametrize("kind", ["tangent_grid", "radius_spread", "far_offset"])
+def test_culling_bvh_exact_on_adversarial_scenes(kind):
+    sd = _random_scene(kind, 7)
+    out = []
+    for variant in (1, 4):
+        r = scenes.make_renderer(sd)
+        r.set_params(variant=variant)
+        r.draw_frames(sd.frames, 1000, 10)
+        out.append((r.read_image(), r.stats()))
+    np.testing.assert_array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
+    assert out[0][1].queries == out[1][1].queries
+    assert out[1][1].variant == 4 and out[1][1].sphere_tests < out[0][1].sphere_tests
+    ref, q = scenes.oracle_render(sd)
+    assert_parity(out[1][0], ref, f"{kind} BVH vs oracle")
+
+
+def test_culling_bvh_with_zero_radius_slots():
+    """The reference's 100-slot buffer: zero-radius slots at the origin inside the BVH (r_min = 0)."""
+    sd = scenes.golden_scene("complex_scene", 96, 64)
+    sd.frames = 6
+    out = []
+    for variant in (1, 4):
+        r = scenes.make_renderer(sd)  # 25 spheres + 75 zero slots = 100 slots
+        r.set_params(variant=variant)
+        r.draw_frames(sd.frames, 1000, 10)
+        out.append(r.read_image())
+    np.testing.assert_array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
 def test_suzanne_tris_mode_vs_oracle():
