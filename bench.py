@@ -32,6 +32,7 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak with packed FMA (MI355X_MICR
 HBM_PEAK_GBS = 8000.0
 SPHERE_TEST_FLOP = 18  # per ray-sphere test (a, 4a hoisted per query)
 BOX_TEST_FLOP = 12  # per padded slab test: 6 adds + 6 multiplies
+RAY_OVERHEAD_FLOP = 90  # ~40 hit reconstruction + ~50 scatter per ray
 
 
 def log(msg: str) -> None:
@@ -161,16 +162,17 @@ def main() -> int:
     if rank == 0:
         value = total_q / t_max / 1e6
         # roofline of the render kernel on rank 0: algorithmic FLOPs per launch / HIP-event launch time.
-        # FLOPs are the tests the kernel actually ran (exact counters): 18 per ray-sphere test (SURVEY
-        # 8(d)), 12 per padded box test (6 sub + 6 mul); brute_force_equiv prices the reference algorithm
-        # (every slot for every ray) at the same time.
+        # Algorithmic = SURVEY 8(d)'s per-ray figure (18 FLOP per slot + ~90 for hit record and scatter)
+        # x rays. executed = the tests the kernel actually ran (exact counters): 18 per ray-sphere test,
+        # 12 per padded box test — with the culling BVH the two differ by ~30x.
         my_q, my_ms, my_launches = float(all_t[0, 1]), float(all_t[0, 2]), float(all_t[0, 3])
         my_box, my_sph = float(all_t[0, 4]), float(all_t[0, 5])
         nl = max(my_launches, 1.0)
         avg_launch_ms = my_ms / nl
-        flop_per_launch = (SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box) / nl
+        flop_per_launch = (SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP) * my_q / nl
         achieved = flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
-        brute_equiv = SPHERE_TEST_FLOP * nslots * my_q / nl / (avg_launch_ms * 1e-3) / 1e12
+        executed = ((SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q) / nl
+                    / (avg_launch_ms * 1e-3) / 1e12)
         px = local_rows * sd.width
         alg_bytes = 24.0 * px + 64.0 * nslots  # framebuffer read+write per launch + sphere arrays
         traffic = None
@@ -214,7 +216,9 @@ def main() -> int:
                 "kernel": f"k_render<sphere, scan variant {variant}>",
                 "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),
                 "box_tests_per_ray": round(my_box / max(my_q, 1.0), 3),
-                "brute_force_equiv_tflops": round(brute_equiv, 3),
+                "executed_tflops": round(executed, 3),
+                "executed_frac": round(executed / FP32_PEAK_TFLOPS, 4),
+                "algorithmic_flop_per_ray": SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP,
                 "avg_launch_ms": round(avg_launch_ms, 3),
                 "flop_per_launch": flop_per_launch,
                 "alg_hbm_bytes_per_launch": alg_bytes,
