@@ -33,6 +33,8 @@ HBM_PEAK_GBS = 8000.0
 SPHERE_TEST_FLOP = 18  # per ray-sphere test (a, 4a hoisted per query)
 BOX_TEST_FLOP = 12  # per padded slab test: 6 adds + 6 multiplies
 RAY_OVERHEAD_FLOP = 90  # ~40 hit reconstruction + ~50 scatter per ray
+NODE_TEST_FLOP = 27  # implicit-heap slab test (3 rcp-mul pairs, mins/maxes)
+TRI_TEST_FLOP = 51  # Moller-Trumbore
 
 
 def log(msg: str) -> None:
@@ -63,9 +65,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--frames", type=int, default=1024, help="spp per step (BASELINE: 1024)")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config (c3 = the headline metric)")
+    ap.add_argument("--frames", type=int, default=None, help="spp per step (default: the config's)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--frames-per-launch", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0,
                     help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
@@ -96,7 +100,11 @@ def main() -> int:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    sd = scenes.config_c3(args.width, args.height, args.frames)
+    sd = scenes.CONFIGS[args.config]()
+    if args.width or args.height or args.frames:
+        sd.width = args.width or sd.width
+        sd.height = args.height or sd.height
+        sd.frames = args.frames or sd.frames
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
     r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant)
@@ -134,6 +142,8 @@ def main() -> int:
     launches = 0
     box_tests = 0
     sphere_tests = 0
+    node_tests = 0
+    tri_tests = 0
     variant = 0
     for i in range(args.steps):
         st = step()
@@ -142,6 +152,8 @@ def main() -> int:
         launches += st.launches
         box_tests += st.box_tests
         sphere_tests += st.sphere_tests
+        node_tests += st.node_tests
+        tri_tests += st.tri_tests
         variant = st.variant
         log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernel {st.kernel_ms:.1f} ms, "
             f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
@@ -149,7 +161,8 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
 
     stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches), float(box_tests),
-                            float(sphere_tests)], dtype=torch.float64, device=dev)
+                            float(sphere_tests), float(node_tests), float(tri_tests)], dtype=torch.float64,
+                           device=dev)
     if dist is not None:
         all_t = [torch.zeros_like(stats_t) for _ in range(world)]
         dist.all_gather(all_t, stats_t)
@@ -167,12 +180,15 @@ def main() -> int:
         # 12 per padded box test — with the culling BVH the two differ by ~30x.
         my_q, my_ms, my_launches = float(all_t[0, 1]), float(all_t[0, 2]), float(all_t[0, 3])
         my_box, my_sph = float(all_t[0, 4]), float(all_t[0, 5])
+        my_nodes, my_tris = float(all_t[0, 6]), float(all_t[0, 7])
         nl = max(my_launches, 1.0)
         avg_launch_ms = my_ms / nl
-        flop_per_launch = (SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP) * my_q / nl
+        # the triangle program runs the reference's own walk: its node/triangle tests are algorithmic as is
+        tri_flop = NODE_TEST_FLOP * my_nodes + TRI_TEST_FLOP * my_tris
+        flop_per_launch = ((SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP) * my_q + tri_flop) / nl
         achieved = flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
-        executed = ((SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q) / nl
-                    / (avg_launch_ms * 1e-3) / 1e12)
+        executed = ((SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q + tri_flop)
+                    / nl / (avg_launch_ms * 1e-3) / 1e12)
         px = local_rows * sd.width
         alg_bytes = 24.0 * px + 64.0 * nslots  # framebuffer read+write per launch + sphere arrays
         traffic = None
@@ -183,7 +199,8 @@ def main() -> int:
             except Exception:  # noqa: BLE001
                 traffic = None
         out = {
-            "metric": "Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)",
+            "metric": ("Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)" if args.config == "c3"
+                       else f"Mrays/sec, {sd.name} {sd.width}x{sd.height}x{sd.frames}spp x {sd.bounces}-bounce"),
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -216,6 +233,8 @@ def main() -> int:
                 "kernel": f"k_render<sphere, scan variant {variant}>",
                 "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),
                 "box_tests_per_ray": round(my_box / max(my_q, 1.0), 3),
+                "tri_node_tests_per_ray": round(my_nodes / max(my_q, 1.0), 3),
+                "tri_tests_per_ray": round(my_tris / max(my_q, 1.0), 3),
                 "executed_tflops": round(executed, 3),
                 "executed_frac": round(executed / FP32_PEAK_TFLOPS, 4),
                 "algorithmic_flop_per_ray": SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP,

@@ -218,9 +218,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         int rc = upload_spheres(r);  // empty scene: min_sphere_slots zero slots, like an unwritten buffer
         if (rc) return rc;
     }
-    int rc = ensure(r->counter, 4);
+    int rc = ensure(r->counter, 8);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, 4 * sizeof(unsigned long long), r->stream));
+    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, 8 * sizeof(unsigned long long), r->stream));
 
     hrt_dev::KParams P{};
     const hrt::Camera& c = r->camera;
@@ -300,12 +300,14 @@ int finish_stats(rt_renderer* r) {
     HIP_TRY(hipEventSynchronize(r->ev_stop));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
-    unsigned long long q[4] = {0, 0, 0, 0};
+    unsigned long long q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpy(q, r->counter.ptr, sizeof(q), hipMemcpyDeviceToHost));
     r->stats.kernel_ms = ms;
     r->stats.queries = q[0];
     r->stats.box_tests = q[1];
     r->stats.sphere_tests = q[2];
+    r->stats.node_tests = q[3];
+    r->stats.tri_tests = q[4];
     r->stats.variant = (uint32_t)r->last_variant;
     r->timing_pending = false;
     return RT_OK;
@@ -385,7 +387,7 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
-    if (p->variant > 4) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->variant > 5) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;

@@ -57,6 +57,7 @@ constexpr int SCAN_SIMPLE = 1;  // one slot per iteration, exact sqrt/div whenev
 constexpr int SCAN_PACKED = 2;  // slot pairs, packed math, interval filter, exact sqrt/div only on ambiguity
 constexpr int SCAN_DEFER = 3;   // slot pairs, packed math, candidate list in LDS, exact resolution after
 constexpr int SCAN_BVH = 4;     // conservative BVH culling + exact tests, (t, slot) lexicographic min
+constexpr int SCAN_BVH_WW = 5;  // the same BVH, while-while traversal (leaves postponed wave-wide)
 constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
 constexpr int BVH_STACK = 24;   // traversal stack entries per lane (LDS); overflow -> exact full scan
 

@@ -207,7 +207,8 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
 }
 
 struct Tally {
-    uint32_t boxes = 0, spheres = 0;
+    uint32_t boxes = 0, spheres = 0;  // sphere culling BVH box tests, ray-sphere tests
+    uint32_t nodes = 0, tris = 0;     // triangle program: implicit-heap node tests, triangle tests
 };
 
 // (t, slot) lexicographic minimum = the reference's linear scan: strict `t < best` keeps the first slot
@@ -323,6 +324,99 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     return bi;
 }
 
+// Variant 5: the same culling BVH and exactness argument as scan_spheres_bvh, traversed "while-while"
+// (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps walking internal nodes until every
+// lane of the wave holds a leaf (or has nothing left), then the wave tests leaves together. This keeps the
+// internal-node and leaf code paths from both running in nearly every iteration.
+constexpr uint32_t BVH_DONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ int scan_spheres_bvh_ww(const KParams& P, const Ray& r, float& best, uint32_t* stack,
+                                                   Tally& tally) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
+    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    float bt = best;
+    int bi = -1;
+    for (uint32_t k = 0; k < P.nlarge; k++) {
+        const int i = P.large_slots[k];
+        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
+        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+    }
+    tally.spheres += P.nlarge;
+
+    const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
+    const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
+    const float D = dl * 1.001f + P.bvh_rr;
+    const float dn = __builtin_amdgcn_sqrtf(a);
+    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
+    const float pad = 2.02f * delta;
+    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+
+    uint32_t node = P.bvh_root, leaf = 0;
+    int sp = 0;
+    bool overflow = false;
+    auto pop = [&]() -> uint32_t { return sp > 0 ? stack[(--sp) * 256] : BVH_DONE; };
+    while (true) {
+        // internal-node phase
+        while (true) {
+            while (node != BVH_DONE && (node & BVH_LEAF_BIT) && leaf == 0) {  // postpone a leaf
+                leaf = node;
+                node = pop();
+            }
+            const bool internal = node != BVH_DONE && !(node & BVH_LEAF_BIT);
+            if (__all(!internal || leaf != 0)) break;  // every lane holds a leaf or cannot descend
+            if (internal) {
+                const float4 n0 = P.bvh_nodes[4 * node + 0];
+                const float4 n1 = P.bvh_nodes[4 * node + 1];
+                const float4 n2 = P.bvh_nodes[4 * node + 2];
+                const float4 n3 = P.bvh_nodes[4 * node + 3];
+                float tl, tr;
+                const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
+                const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
+                tally.boxes += 2;
+                const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
+                    else overflow = true;
+                    node = lfirst ? left : right;
+                } else if (hl) {
+                    node = left;
+                } else if (hr) {
+                    node = right;
+                } else {
+                    node = pop();
+                }
+            }
+        }
+        // leaf phase
+        if (leaf != 0) {
+            const uint32_t first = (leaf >> 4) & 0x07FFFFFFu, cnt = leaf & 15u;
+            for (uint32_t j = 0; j < cnt; j++) {
+                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
+                const int i = P.bvh_slot[first + j];
+                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+            }
+            tally.spheres += cnt;
+            leaf = 0;
+        }
+        if (__all(node == BVH_DONE)) break;
+    }
+    if (overflow) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    best = bt;
+    return bi;
+}
+
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
     const f3 p = point_on_ray(r.o, r.d, t);
@@ -376,18 +470,22 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
 }
 
 // intersect_all_node (shader_tris.wgsl:268-301): stackless DFS over the implicit heap, 600-step cap.
-__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h) {
+__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h, Tally& tally) {
     const f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const uint32_t n = P.n, m = P.m;
     uint32_t i = 1;
     for (int step = 0; step < 600; step++) {
-        if (i < n && node_hit(P, i, r.o, inv)) {
-            i *= 2u;
-            continue;
+        if (i < n) {
+            tally.nodes++;
+            if (node_hit(P, i, r.o, inv)) {
+                i *= 2u;
+                continue;
+            }
         }
         if (i >= n) {
             const uint32_t j = i - n;
             if (j >= m) break;
+            tally.tris++;
             tri_test(P, r, j, h);
         }
         i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
@@ -402,7 +500,9 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
         int bi;
-        if constexpr (SCAN == SCAN_BVH) {
+        if constexpr (SCAN == SCAN_BVH_WW) {
+            bi = scan_spheres_bvh_ww(P, r, best, (uint32_t*)lds, tally);
+        } else if constexpr (SCAN == SCAN_BVH) {
             bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_DEFER) {
             bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
@@ -416,7 +516,7 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
         }
         if (bi >= 0) sphere_record(P, r, bi, best, h);
     }
-    if (MODE != MODE_SPHERE) walk_bvh(P, r, h);
+    if (MODE != MODE_SPHERE) walk_bvh(P, r, h, tally);
     // abs(hit.t - FLT_MAX) < EPSILON (shader_sphere.wgsl:235): t is FLT_MAX_REF exactly or >= 2^103 away.
     return h.t != FLT_MAX_REF;
 }
@@ -513,7 +613,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
-    } else if constexpr (SCAN == SCAN_BVH) {
+    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVH_WW) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
         lds_list = bvh_stack + threadIdx.x;
     }
@@ -582,18 +682,17 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         px[1] = acc1;
         px[2] = acc2;
     }
-    // One atomic per wave and counter: rays, box tests, exact sphere tests.
-    unsigned long long qsum = queries, bsum = tally.boxes, ssum = tally.spheres;
+    // One atomic per wave and counter: rays, box tests, sphere tests, tri-program node and triangle tests.
+    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        qsum += __shfl_xor(qsum, off);
-        bsum += __shfl_xor(bsum, off);
-        ssum += __shfl_xor(ssum, off);
+    for (int c = 0; c < 5; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
     if (lane == 0) {
-        if (qsum) atomicAdd(P.counter, qsum);
-        if (bsum) atomicAdd(P.counter + 1, bsum);
-        if (ssum) atomicAdd(P.counter + 2, ssum);
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
     }
 }
 
@@ -608,6 +707,7 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_SIMPLE>), grid, block, 0, stream, P);
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_PACKED>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_WW>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
@@ -615,6 +715,7 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_SIMPLE>), grid, block, 0, stream, P);
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_PACKED>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_WW>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     }

@@ -49,6 +49,8 @@ class RtStats(C.Structure):
         ("sphere_tests", C.c_uint64),
         ("variant", C.c_uint32),
         ("pad0", C.c_uint32),
+        ("node_tests", C.c_uint64),
+        ("tri_tests", C.c_uint64),
     ]
 
 

@@ -73,8 +73,10 @@ typedef struct rt_stats {
     uint32_t local_rows;   /* rows owned by this renderer                                              */
     uint64_t box_tests;    /* padded-box tests of the sphere culling BVH (variant 4), last draw call    */
     uint64_t sphere_tests; /* ray-sphere tests (slots scanned, or BVH leaf + large-list tests)          */
-    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..4)                         */
+    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..5)                         */
     uint32_t pad0;
+    uint64_t node_tests;   /* triangle program: implicit-heap node (slab) tests                         */
+    uint64_t tri_tests;    /* triangle program: Moller-Trumbore tests                                   */
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

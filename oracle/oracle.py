@@ -38,7 +38,8 @@ def lib() -> C.CDLL:
         L = C.CDLL(os.fspath(LIB))
         L.oracle_render.restype = C.c_uint64
         L.oracle_render.argtypes = [C.POINTER(OParams), C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
-                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                    C.POINTER(C.c_uint64)]
         L.oracle_sizeof.restype = C.c_uint32
         L.oracle_sizeof.argtypes = [C.c_int]
         assert [L.oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
@@ -94,6 +95,12 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
     cam = np.ascontiguousarray(camera).tobytes()
     if threads <= 0:  # explicit: importing torch can leave the OpenMP default at one thread
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    counts = (C.c_uint64 * 3)()
     q = lib().oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
-                            image.ctypes.data, threads)
+                            image.ctypes.data, threads, counts)
+    last_counts.update(rays=counts[0], node_tests=counts[1], tri_tests=counts[2])
     return image, int(q)
+
+
+# {rays, node_tests, tri_tests} of the last render() call (triangle-program work counters)
+last_counts: dict = {}

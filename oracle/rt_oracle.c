@@ -13,7 +13,7 @@
  *
  * Pinning: the reference is Rust + WGSL run through wgpu; there is no Rust toolchain, no wgpu and no
  * GPU here, so it cannot be built. This restatement is pinned by the reference's
- * own golden images (tests/rendering_tests.rs:134-509, tests/golden/*.ppm): >= 99.9 % of u8 channels
+ * own golden images (tests/rendering_tests.rs:134-509, tests/golden/NAME.ppm): >= 99.9 % of u8 channels
  * bit-exact on the five non-glass scenes, harness metric (mean |du8| <= 2 % of 255) on all seven.
  * The triangle/BVH path has no image golden in the reference: it is pinned structurally only
  * (bvh/tree.rs:93-126) — "parity unpinned" at image level for tris mode.
@@ -197,16 +197,20 @@ static inline void tri_test(const o_scene *sc, ray_t r, uint32_t j, hit_t *h) {
 }
 
 /* intersect_all_node: shader_tris.wgsl:268-301 — stackless walk of the implicit heap, 600-step cap */
-static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h) {
+static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h, uint64_t *cnt) {
     v3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     uint32_t i = 1, n = sc->n, m = sc->m;
     int step = 0;
     while (step < 600) {
         step++;
-        if (i < n && node_hit(r.o, inv, &sc->nodes[i])) { i *= 2u; continue; }
+        if (i < n) {
+            cnt[1]++; /* node (slab) tests */
+            if (node_hit(r.o, inv, &sc->nodes[i])) { i *= 2u; continue; }
+        }
         if (i >= n) {
             uint32_t j = i - n;
             if (j >= m) break;
+            cnt[2]++; /* triangle tests */
             tri_test(sc, r, j, h);
         }
         while ((i & 1u) == 1u) i /= 2u;
@@ -260,14 +264,14 @@ static ray_t scatter(const o_scene *sc, uint32_t *s, ray_t r, const hit_t *h) {
 }
 
 /* trace: shader_sphere.wgsl:230-243 / shader_tris.wgsl:303-316 */
-static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *queries) {
+static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *cnt) {
     v3 att = V(1.0f, 1.0f, 1.0f);
     ray_t cur = primary;
     for (uint32_t b = 0; b < sc->bounces; b++) {
         hit_t h = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, FLT_MAX_REF, 0, 0};
         if (sc->mode != MODE_TRIS) closest_sphere(sc, cur, &h);
-        if (sc->mode != MODE_SPHERE) closest_bvh(sc, cur, &h);
-        (*queries)++;
+        if (sc->mode != MODE_SPHERE) closest_bvh(sc, cur, &h, cnt);
+        cnt[0]++; /* closest-hit queries (rays) */
         if (fabsf(h.t - FLT_MAX_REF) < sc->eps) break;
         cur = scatter(sc, s, cur, &h);
         const float *al = h.mat->albedo;
@@ -280,7 +284,7 @@ static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *queries
 
 /* fs_main: shader_sphere.wgsl:251-273 — one pixel, one frame */
 static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, uint32_t y, uint32_t time,
-                       uint64_t *queries) {
+                       uint64_t *cnt) {
     uint32_t s = (x * H + y) * time;
     float aspect = (float)W / (float)H;
     float r1 = rng_float(&s), r2 = rng_float(&s);
@@ -291,7 +295,7 @@ static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, ui
     ux = (2.0f * ux - 1.0f) * aspect;
     uy = (2.0f * uy - 1.0f) * -1.0f;
     ray_t r = make_ray(sc, ux, uy, &s);
-    v3 c = trace(sc, r, &s, queries);
+    v3 c = trace(sc, r, &s, cnt);
     return V(0.0f + c.x, 0.0f + c.y, 0.0f + c.z);
 }
 
@@ -299,11 +303,12 @@ static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, ui
  * oracle_render: draw p->frames frames into `image` (rows k < nrows, columns x0..x0+nx, RGB f32,
  * layout ((k*nx) + (x-x0))*3), continuing the accumulation already in `image` exactly as
  * repeated Renderer::draw() calls do (renderer.rs:355-410, accumulation at shader_sphere.wgsl:264-271).
- * Returns the number of closest-hit queries (rays) traced.
+ * Returns the number of closest-hit queries (rays) traced; if `counts` is given it receives
+ * {rays, triangle-program node tests, triangle tests}.
  */
 uint64_t oracle_render(const o_params *p, const void *camera80, const void *spheres48, uint32_t nslots,
                        const uint32_t *sizes, const void *nodes32, const void *tris64, const void *mats32,
-                       float *image, int threads) {
+                       float *image, int threads, uint64_t *counts) {
     o_scene sc;
     sc.cam = (const o_camera *)camera80;
     sc.k = tanf(sc.cam->params[2] * 0.5f);
@@ -312,21 +317,21 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
     sc.n = sizes ? sizes[0] : 0; sc.m = sizes ? sizes[1] : 0;
     sc.mode = p->mode; sc.bounces = p->bounces;
     sc.eps = p->mode == MODE_SPHERE ? 1e-6f : 1e-4f;
-    uint64_t total = 0;
+    uint64_t total = 0, tnodes = 0, ttris = 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, tnodes, ttris)
 #endif
     for (int64_t k = 0; k < (int64_t)p->nrows; k++) {
         uint32_t y = p->row0 + (uint32_t)k * p->row_step;
-        uint64_t q = 0;
+        uint64_t q[3] = {0, 0, 0};
         for (uint32_t x = p->x0; x < p->x0 + p->nx; x++) {
             float *px = image + ((size_t)k * p->nx + (x - p->x0)) * 3;
             float r = px[0], g = px[1], b = px[2];
             for (uint32_t f = 0; f < p->frames; f++) {
                 uint32_t fc = p->frame0 + f;
                 uint32_t time = p->time0 + f * p->dtime;
-                v3 c = sample_pixel(&sc, p->width, p->height, x, y, time, &q);
+                v3 c = sample_pixel(&sc, p->width, p->height, x, y, time, q);
                 float w = 1.0f / (fminf((float)fc, (float)p->ema_cap) + 1.0f);
                 r = r * (1.0f - w) + c.x * w;
                 g = g * (1.0f - w) + c.y * w;
@@ -334,7 +339,14 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
             }
             px[0] = r; px[1] = g; px[2] = b;
         }
-        total += q;
+        total += q[0];
+        tnodes += q[1];
+        ttris += q[2];
+    }
+    if (counts) {
+        counts[0] = total;
+        counts[1] = tnodes;
+        counts[2] = ttris;
     }
     return total;
 }

@@ -220,6 +220,17 @@ def config_c4(width: int = 1920, height: int = 1080, frames: int = 512) -> Scene
                     bounces=50, min_sphere_slots=0)
 
 
+def config_c5(width: int = 3840, height: int = 2160, frames: int = 4096) -> SceneDef:
+    """C5: the C3 cover scene plus suzanne.obj (979 triangles, mesh at its file coordinates), mixed mode,
+    3840x2160, 4096 spp, 50 bounces (BASELINE: row tiles across 8 GPUs)."""
+    bvh = suzanne_tree().view()
+    return SceneDef("C5-rtiow-suzanne-4k", hrt.RT_MODE_MIXED, width, height, rtiow_camera(), rtiow_spheres(),
+                    bvh=bvh, frames=frames, bounces=50, min_sphere_slots=0)
+
+
+CONFIGS = {"c1": config_c1, "c2": config_c2, "c3": config_c3, "c4": config_c4, "c5": config_c5}
+
+
 def make_renderer(sd: SceneDef) -> "hrt.Renderer":
     """GPU renderer loaded with a SceneDef (camera, buffers, params)."""
     r = hrt.Renderer(sd.width, sd.height, sd.mode)

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_layouts_match_header():
     assert C.sizeof(hrt.RtParams) == 7 * 4
-    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4
+    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
 
