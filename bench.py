@@ -73,6 +73,9 @@ def main() -> int:
     ap.add_argument("--frames-per-launch", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0,
                     help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    ap.add_argument("--verify", action="store_true", help="rank 0 re-renders the image alone and compares")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=64)
@@ -94,8 +97,13 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one rank per GPU; (rehearsal only: more ranks than GPUs share devices, with --backend gloo)
+        dev_index = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        if args.backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -162,7 +170,7 @@ def main() -> int:
 
     stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches), float(box_tests),
                             float(sphere_tests), float(node_tests), float(tri_tests)], dtype=torch.float64,
-                           device=dev)
+                           device=dev if args.backend == "nccl" else "cpu")
     if dist is not None:
         all_t = [torch.zeros_like(stats_t) for _ in range(world)]
         dist.all_gather(all_t, stats_t)
@@ -247,6 +255,15 @@ def main() -> int:
         if not args.no_cpu_baseline and world == 1:
             log("cpu baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline(sd, min(16, os.cpu_count() or 1), args.cpu_rows, args.cpu_frames)
+        if args.verify:
+            # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
+            ref_r = scenes.make_renderer(sd)
+            ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant)
+            ref_r.draw_frames(sd.frames, 1000, 10)
+            ref_img = torch.from_numpy(ref_r.read_image())
+            same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))
+            out["verify_gather_bitwise"] = bool(same)
+            log(f"verify: gathered image {'==' if same else '!='} single-renderer image")
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

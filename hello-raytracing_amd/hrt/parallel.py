@@ -33,6 +33,14 @@ def gather_image(part, height: int, dist, rank: int, world: int, dst: int = 0, g
 
     if world == 1:
         return part[:height] if out is None else out.copy_(part[:height])
+    if dist.get_backend() == "gloo" and part.is_cuda:  # gloo has no device gather: stage through the host
+        host = part.cpu()
+        hg = [torch.empty_like(host) for _ in range(world)] if rank == dst else None
+        dist.gather(host, hg, dst=dst)
+        if rank != dst:
+            return None
+        full = assemble(hg, height, world)
+        return full.to(part.device) if out is None else out.copy_(full)
     if rank == dst and gathered is None:
         gathered = [torch.empty_like(part) for _ in range(world)]
     dist.gather(part, gathered if rank == dst else None, dst=dst)
