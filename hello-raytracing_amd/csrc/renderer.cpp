@@ -112,6 +112,7 @@ struct rt_renderer {
     rt_stats stats{};
     bool timing_pending = false;
     int last_variant = 0;
+    unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
@@ -218,9 +219,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         int rc = upload_spheres(r);  // empty scene: min_sphere_slots zero slots, like an unwritten buffer
         if (rc) return rc;
     }
-    int rc = ensure(r->counter, 8);
+    int rc = ensure(r->counter, RT_RAW_COUNTERS);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, 8 * sizeof(unsigned long long), r->stream));
+    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, RT_RAW_COUNTERS * sizeof(unsigned long long), r->stream));
 
     hrt_dev::KParams P{};
     const hrt::Camera& c = r->camera;
@@ -272,7 +273,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.pad_k2 = B.r_min > 0.0f ? 16.0f * u / B.r_min : INFINITY;
     P.pad_k3 = 2e-3f;
     P.pad_k4 = 4.0f * u;
-    const int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
+    int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
+    // the lane state machine is sphere-program only and needs at least one bounce
+    if (variant == hrt_dev::SCAN_LANES && (r->mode != RT_MODE_SPHERE || P.bounces == 0)) variant = hrt_dev::SCAN_BVH;
+    // the LDS copy of the BVH holds at most BVH_LDS_NODES nodes
+    P.bvh_nnodes = (uint32_t)B.nodes.size();
+    if (variant == hrt_dev::SCAN_BVH_LDS && P.bvh_nnodes > (uint32_t)hrt_dev::BVH_LDS_NODES) variant = hrt_dev::SCAN_BVH;
     r->last_variant = variant;
 
     const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
@@ -300,8 +306,8 @@ int finish_stats(rt_renderer* r) {
     HIP_TRY(hipEventSynchronize(r->ev_stop));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
-    unsigned long long q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpy(q, r->counter.ptr, sizeof(q), hipMemcpyDeviceToHost));
+    unsigned long long* q = r->raw_counters;
+    HIP_TRY(hipMemcpy(q, r->counter.ptr, RT_RAW_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     r->stats.kernel_ms = ms;
     r->stats.queries = q[0];
     r->stats.box_tests = q[1];
@@ -387,7 +393,7 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
-    if (p->variant > 5) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->variant > 8) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;
@@ -537,6 +543,22 @@ int rt_get_stats(const rt_renderer* r, rt_stats* out) {
     if (rc) return rc;
     *out = r->stats;
     return RT_OK;
+}
+
+int rt_get_raw_counters(const rt_renderer* r, uint64_t* out, int n) {
+    if (!r || !out || n < 0) return fail(RT_ERR_ARG, "rt_get_raw_counters: bad argument");
+    int rc = finish_stats(const_cast<rt_renderer*>(r));
+    if (rc) return rc;
+    for (int i = 0; i < n; i++) out[i] = i < RT_RAW_COUNTERS ? r->raw_counters[i] : 0;
+    return RT_OK;
+}
+
+int rt_diagnostic_build(void) {
+#ifdef HRT_STAMPS
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 }  // extern "C"

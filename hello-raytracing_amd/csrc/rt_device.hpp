@@ -58,6 +58,12 @@ constexpr int SCAN_PACKED = 2;  // slot pairs, packed math, interval filter, exa
 constexpr int SCAN_DEFER = 3;   // slot pairs, packed math, candidate list in LDS, exact resolution after
 constexpr int SCAN_BVH = 4;     // conservative BVH culling + exact tests, (t, slot) lexicographic min
 constexpr int SCAN_BVH_WW = 5;  // the same BVH, while-while traversal (leaves postponed wave-wide)
+constexpr int SCAN_LANES = 6;   // the same BVH, per-lane state machine with batched shading (sphere mode)
+constexpr int SCAN_BVH_LDS = 7; // variant 4 with the BVH nodes staged in LDS per workgroup
+constexpr int BVH_LDS_NODES = 320;  // node capacity of the LDS copy (20 KB)
+constexpr int BVH_STACK_LDS = 12;   // stack entries per lane for variant 7 (overflow -> exact full scan)
+constexpr int SCAN_BVH_CULL = 8;    // variant 4 + popped subtrees re-culled against the current best t
+constexpr int BVH_STACK_CULL = 12;  // (node word, entry distance) pairs per lane for variant 8
 constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
 constexpr int BVH_STACK = 24;   // traversal stack entries per lane (LDS); overflow -> exact full scan
 
@@ -84,6 +90,7 @@ struct KParams {
     const int* bvh_slot;          // original slot of each leaf sphere
     const int* large_slots;       // slots scanned linearly for every ray
     uint32_t nlarge, bvh_root;    // large-list length, root child word
+    uint32_t bvh_nnodes;          // internal nodes (4 float4 each)
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     const float4* nodes;          // 2 float4 per node: min, max

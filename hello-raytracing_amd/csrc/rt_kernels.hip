@@ -25,6 +25,18 @@ struct Ray {
     f3 o, d;
 };
 
+#ifdef HRT_STAMPS
+// In-kernel stamp (diagnostic build): one s_memtime with its wait inside the statement, fenced from
+// scheduling (cdna_hip_programming.md §7, In-kernel stamps).
+__device__ __forceinline__ unsigned long long hrt_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
+
 struct Hit {
     f3 p, n;
     float t;
@@ -251,8 +263,14 @@ __device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx,
 // visited sphere is tested with the reference arithmetic, and the winner is the (t, slot) minimum.
 // Rays the bound does not cover (non-finite origin, 2a outside [2^-100, 2^100]) or a stack overflow fall
 // back to the full exact scan.
+// `nodes` is P.bvh_nodes (global) or the workgroup's LDS copy of it (variant 7); `stack_cap` the per-lane
+// LDS stack depth.
+// CULL_POP: every stack entry also keeps the padded-box entry distance of its subtree (second half of the
+// stack area), and a popped subtree whose entry already exceeds the current best t is skipped without
+// loading it — the same strict `entry > best` criterion the visit test applies, so still exact.
+template <int STACK_CAP = BVH_STACK, bool CULL_POP = false>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
-                                                Tally& tally) {
+                                                Tally& tally, const float4* __restrict__ nodes) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a;
     const float a2 = 2.0f * a;
@@ -286,10 +304,10 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     bool overflow = false;
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
-            const float4 n0 = P.bvh_nodes[4 * node + 0];
-            const float4 n1 = P.bvh_nodes[4 * node + 1];
-            const float4 n2 = P.bvh_nodes[4 * node + 2];
-            const float4 n3 = P.bvh_nodes[4 * node + 3];
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
             float tl, tr;
             const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
             const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
@@ -297,8 +315,13 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
-                if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
-                else overflow = true;
+                if (sp < STACK_CAP) {
+                    stack[sp * 256] = lfirst ? right : left;
+                    if constexpr (CULL_POP) stack[(STACK_CAP + sp) * 256] = __float_as_uint(lfirst ? tr : tl);
+                    sp++;
+                } else {
+                    overflow = true;
+                }
                 node = lfirst ? left : right;
                 continue;
             }
@@ -313,8 +336,21 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             }
             tally.spheres += cnt;
         }
-        if (sp == 0) break;
-        node = stack[(--sp) * 256];
+        if constexpr (CULL_POP) {
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                if (__uint_as_float(stack[(STACK_CAP + sp) * 256]) <= bt) {
+                    node = stack[sp * 256];
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+        } else {
+            if (sp == 0) break;
+            node = stack[(--sp) * 256];
+        }
     }
     if (overflow) {
         tally.spheres += P.nslots;
@@ -495,7 +531,8 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h,
 }
 
 template <int MODE, int SCAN>
-__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally) {
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally,
+                                            const float4* lds_nodes) {
     h.t = FLT_MAX_REF;
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
@@ -503,7 +540,11 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
         if constexpr (SCAN == SCAN_BVH_WW) {
             bi = scan_spheres_bvh_ww(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_BVH) {
-            bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
+            bi = scan_spheres_bvh<BVH_STACK>(P, r, best, (uint32_t*)lds, tally, P.bvh_nodes);
+        } else if constexpr (SCAN == SCAN_BVH_LDS) {
+            bi = scan_spheres_bvh<BVH_STACK_LDS>(P, r, best, (uint32_t*)lds, tally, lds_nodes);
+        } else if constexpr (SCAN == SCAN_BVH_CULL) {
+            bi = scan_spheres_bvh<BVH_STACK_CULL, true>(P, r, best, (uint32_t*)lds, tally, P.bvh_nodes);
         } else if constexpr (SCAN == SCAN_DEFER) {
             bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
             tally.spheres += P.nslots;
@@ -535,17 +576,19 @@ __device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
 }
 
 // scatter (shader_sphere.wgsl:172-217; shader_tris.wgsl:222-267 reflects the raw direction for metal).
+// The three material arms share code so a wave holding several materials runs one hemisphere sample and
+// one final normalize instead of one per arm; every lane still performs exactly its own arm's operations
+// (and RNG draws) in the reference's order, so results are unchanged.
 template <int MODE>
 __device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
-    f3 d;
-    if (h.id == 1u) {
-        d = random_on_hemisphere<MODE>(s, h.n);
-    } else if (h.id == 2u) {
+    const bool lambert = h.id == 1u, metal = h.id == 2u;
+    f3 hemi = mk(0.0f, 0.0f, 0.0f);
+    if (lambert || metal) hemi = random_on_hemisphere<MODE>(s, h.n);  // 3 draws, both arms
+    f3 u = hemi;
+    if (metal) {
         const f3 in = MODE == MODE_SPHERE ? normalize(r.d) : r.d;
-        const f3 refl = reflect(in, h.n);
-        const f3 hemi = random_on_hemisphere<MODE>(s, h.n);
-        d = normalize(refl + h.param * hemi);
-    } else {  // MAT_DIELECTRIC and the default arm
+        u = reflect(in, h.n) + h.param * hemi;
+    } else if (!lambert) {  // MAT_DIELECTRIC and the default arm
         float ir = h.param;
         if (h.front) ir = 1.0f / ir;
         const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
@@ -555,10 +598,10 @@ __device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
             const float f = rng_float(s);
             refl = reflectance(cos_t, ir) > (f - __builtin_floorf(f));
         }
-        d = refl ? normalize(reflect(r.d, h.n)) : normalize(refract(r.d, h.n, ir));
+        u = refl ? reflect(r.d, h.n) : refract(r.d, h.n, ir);
     }
     r.o = h.p;
-    r.d = d;
+    r.d = lambert ? hemi : normalize(u);
 }
 
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
@@ -617,6 +660,20 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
         lds_list = bvh_stack + threadIdx.x;
     }
+    if constexpr (SCAN == SCAN_BVH_CULL) {
+        __shared__ uint32_t bvh_stack_c[2 * BVH_STACK_CULL * 256];
+        lds_list = bvh_stack_c + threadIdx.x;
+    }
+    const float4* lds_nodes = nullptr;
+    if constexpr (SCAN == SCAN_BVH_LDS) {
+        // the culling BVH (<= BVH_LDS_NODES nodes, checked by the host) staged once per workgroup
+        __shared__ uint32_t bvh_stack_s[BVH_STACK_LDS * 256];
+        __shared__ float4 nodes_s[4 * BVH_LDS_NODES];
+        lds_list = bvh_stack_s + threadIdx.x;
+        for (uint32_t i = threadIdx.x; i < 4u * P.bvh_nnodes; i += 256u) nodes_s[i] = P.bvh_nodes[i];
+        __syncthreads();
+        lds_nodes = nodes_s;
+    }
     Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
@@ -643,12 +700,23 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         sky_t = ray.d.y * 0.5f + 0.5f;
     }
 
+#ifdef HRT_STAMPS  // diagnostic build only (lib/libhrt_diag.so): wave cycles per region
+    unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb, st_tc;
+    const unsigned long long st_start = hrt_stamp();
+#endif
     while (f < P.nframes) {
         bool done = true;
+#ifdef HRT_STAMPS
+        st_ta = hrt_stamp();
+#endif
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, lds_nodes);
             queries++;
+#ifdef HRT_STAMPS
+            st_tb = hrt_stamp();
+            st_trav += st_tb - st_ta;
+#endif
             if (hit) {
                 scatter<MODE>(s, ray, h);
                 att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
@@ -656,6 +724,10 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
                 done = bounce >= P.bounces;
             }
         }
+#ifdef HRT_STAMPS
+        st_tc = hrt_stamp();
+        st_shade += st_tc - st_tb;
+#endif
         if (done) {
             // trace() epilogue (:241-242) + accumulation (:264-271).
             const float u = 1.0f - sky_t;
@@ -675,6 +747,9 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
                 bounce = 0;
             }
         }
+#ifdef HRT_STAMPS
+        st_gen += hrt_stamp() - st_tc;
+#endif
     }
 
     if (valid) {
@@ -682,7 +757,200 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         px[1] = acc1;
         px[2] = acc2;
     }
+#ifdef HRT_STAMPS
+    if (lane == 0) {
+        atomicAdd(P.counter + 8, st_trav);
+        atomicAdd(P.counter + 9, st_shade);
+        atomicAdd(P.counter + 10, st_gen);
+        atomicAdd(P.counter + 11, hrt_stamp() - st_start);
+    }
+#endif
     // One atomic per wave and counter: rays, box tests, sphere tests, tri-program node and triangle tests.
+    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+    }
+}
+
+// Variant 6 — sphere program with the culling BVH of variant 4, scheduled as a per-lane state machine.
+// Every iteration of the outer loop advances each traversing lane by ONE traversal step (an internal node
+// or a leaf); lanes whose traversal has finished wait, and the wave shades them in a batch (hit record,
+// scatter, accumulation, next sample's primary ray, start of the next query) once at least
+// LANES_SHADE_BATCH lanes wait or nobody is traversing. A lane therefore never idles behind the wave's
+// longest traversal, and the shading code runs for many lanes at once. Per lane the sequence of
+// operations is exactly variant 4's, so the results are bit-identical.
+constexpr int LANES_SHADE_BATCH = 24;
+
+__global__ __launch_bounds__(256) void k_render_lanes(const KParams P) {
+    constexpr int MODE = MODE_SPHERE;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+    uint32_t* stack = bvh_stack + threadIdx.x;
+    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const bool valid = x < P.W && kr < P.nrows;
+    const uint32_t y = P.row0 + kr * P.row_step;
+    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
+    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
+    if (valid) {
+        acc0 = px[0];
+        acc1 = px[1];
+        acc2 = px[2];
+    }
+    Tally tally;
+    uint32_t queries = 0;
+    uint32_t f = 0;
+
+    // path state
+    Ray ray;
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    float sky_t = 0.0f;
+    uint32_t s = 0, bounce = 0;
+    // query / traversal state
+    float a4 = 0.0f, a2 = 0.0f, bt = FLT_MAX_REF;
+    int bi = -1;
+    f3 inv = mk(0, 0, 0), lo = mk(0, 0, 0), hi = mk(0, 0, 0);
+    uint32_t node = BVH_DONE;
+    int sp = 0;
+    bool overflow = false;
+    int state = 2;  // 0 traversing, 1 waiting for shading, 2 finished
+
+    auto begin_query = [&]() {
+        queries++;
+        const float a = dot(ray.d, ray.d);
+        a4 = 4.0f * a;
+        a2 = 2.0f * a;
+        bt = FLT_MAX_REF;
+        bi = -1;
+        const bool finite_o =
+            __builtin_isfinite(ray.o.x) && __builtin_isfinite(ray.o.y) && __builtin_isfinite(ray.o.z);
+        if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {  // outside the padding bound: exact scan
+            bi = scan_spheres(P, ray, bt);
+            tally.spheres += P.nslots;
+            state = 1;
+            return;
+        }
+        for (uint32_t k = 0; k < P.nlarge; k++) {
+            const int i = P.large_slots[k];
+            const float t = exact_t_geo(P.sph_geo[i], ray, a4, a2);
+            if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+        }
+        tally.spheres += P.nlarge;
+        const f3 op = mk(ray.o.x - P.bvh_rc[0], ray.o.y - P.bvh_rc[1], ray.o.z - P.bvh_rc[2]);
+        const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
+        const float D = dl * 1.001f + P.bvh_rr;
+        const float dn = __builtin_amdgcn_sqrtf(a);
+        const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
+        const float pad = 2.02f * delta;
+        inv = mk(robust_inv(ray.d.x), robust_inv(ray.d.y), robust_inv(ray.d.z));
+        lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+        hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+        node = P.bvh_root;
+        sp = 0;
+        overflow = false;
+        state = 0;
+    };
+    auto start_sample = [&]() {
+        ray = primary_ray<MODE>(P, x, y, P.time0 + f * P.dtime, s);
+        sky_t = ray.d.y * 0.5f + 0.5f;
+        att = mk(1.0f, 1.0f, 1.0f);
+        bounce = 0;
+    };
+
+    if (valid && P.nframes > 0) {  // the host routes bounces == 0 to another variant
+        start_sample();
+        begin_query();
+    }
+
+    while (true) {
+        if (state == 0) {  // one traversal step
+            bool finished = false;
+            if (!(node & BVH_LEAF_BIT)) {
+                const float4 n0 = P.bvh_nodes[4 * node + 0];
+                const float4 n1 = P.bvh_nodes[4 * node + 1];
+                const float4 n2 = P.bvh_nodes[4 * node + 2];
+                const float4 n3 = P.bvh_nodes[4 * node + 3];
+                float tl, tr;
+                const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
+                const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
+                tally.boxes += 2;
+                const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
+                    else overflow = true;
+                    node = lfirst ? left : right;
+                } else if (hl) {
+                    node = left;
+                } else if (hr) {
+                    node = right;
+                } else {
+                    finished = sp == 0;
+                    if (!finished) node = stack[(--sp) * 256];
+                }
+            } else {
+                const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const float t = exact_t_geo(P.bvh_sph[first + j], ray, a4, a2);
+                    const int i = P.bvh_slot[first + j];
+                    if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+                }
+                tally.spheres += cnt;
+                finished = sp == 0;
+                if (!finished) node = stack[(--sp) * 256];
+            }
+            if (finished) {
+                if (overflow) {  // stack overflow: exact full scan decides
+                    bt = FLT_MAX_REF;
+                    bi = scan_spheres(P, ray, bt);
+                    tally.spheres += P.nslots;
+                }
+                state = 1;
+            }
+        }
+        const unsigned long long waiting = __ballot(state == 1), walking = __ballot(state == 0);
+        if (!waiting && !walking) break;
+        if (walking && __popcll(waiting) < LANES_SHADE_BATCH) continue;
+        if (state == 1) {  // shade: trace() loop body + fs_main accumulation, then the next query
+            bool done = true;
+            if (bi >= 0) {
+                Hit h;
+                sphere_record(P, ray, bi, bt, h);
+                scatter<MODE>(s, ray, h);
+                att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                bounce++;
+                done = bounce >= P.bounces;
+            }
+            if (done) {
+                const float u = 1.0f - sky_t;
+                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+                const f3 c = att * sky;
+                const float fc = (float)(P.frame0 + f);
+                const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
+                const float omw = 1.0f - w;
+                acc0 = acc0 * omw + (0.0f + c.x) * w;
+                acc1 = acc1 * omw + (0.0f + c.y) * w;
+                acc2 = acc2 * omw + (0.0f + c.z) * w;
+                f++;
+                if (f < P.nframes) start_sample();
+            }
+            if (f < P.nframes) begin_query();
+            else state = 2;
+        }
+    }
+
+    if (valid) {
+        px[0] = acc0;
+        px[1] = acc1;
+        px[2] = acc2;
+    }
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
@@ -708,6 +976,9 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_PACKED>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_WW>), grid, block, 0, stream, P);
+        else if (variant == SCAN_LANES) hipLaunchKernelGGL(k_render_lanes, grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_LDS>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_CULL>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
@@ -716,6 +987,8 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_PACKED>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_WW>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_LDS>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_CULL>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     }

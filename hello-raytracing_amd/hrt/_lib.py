@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent  # hello-raytracing_amd/
-LIB_PATH = PKG_ROOT / "lib" / "libhrt.so"
+# HRT_LIB may name the diagnostic build (lib/libhrt_diag.so, relative to the package) for timing studies.
+LIB_PATH = PKG_ROOT / os.environ.get("HRT_LIB", "lib/libhrt.so")
 
 RT_OK = 0
 RT_ERR_ARG = -1
@@ -79,6 +80,8 @@ SIGNATURES = {
     "rt_resize": (C.c_int, [_P, _U32, _U32]),
     "rt_synchronize": (C.c_int, [_P]),
     "rt_get_stats": (C.c_int, [_P, C.POINTER(RtStats)]),
+    "rt_get_raw_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
+    "rt_diagnostic_build": (C.c_int, []),
     "rt_last_error": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),
     "rt_build_info": (C.c_char_p, []),

@@ -300,6 +300,13 @@ class Renderer:
         check(lib().rt_get_stats(self._h, C.byref(s)), "get_stats")
         return s
 
+    def raw_counters(self, n: int = 16) -> list:
+        """Device counters of the last draw (include/hrt.h rt_get_raw_counters; slots 8-11 are
+        region cycle sums in the diagnostic build)."""
+        buf = (C.c_uint64 * n)()
+        check(lib().rt_get_raw_counters(self._h, buf, n), "get_raw_counters")
+        return list(buf)
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().rt_destroy(self._h)

@@ -122,6 +122,14 @@ int rt_resize(rt_renderer *r, uint32_t width, uint32_t height);
 int rt_synchronize(rt_renderer *r);
 int rt_get_stats(const rt_renderer *r, rt_stats *out);
 
+/* Raw per-draw device counters (no reference counterpart; diagnostics). Slots 0-4 are the rt_stats
+ * work counters; in the diagnostic build (rt_diagnostic_build() == 1, lib/libhrt_diag.so) slots 8-11
+ * hold summed wave clock cycles spent in closest-hit queries, shading, sample generation/accumulation
+ * and whole wave lifetimes. Writes min(n, RT_RAW_COUNTERS) values, zero beyond. */
+#define RT_RAW_COUNTERS 16
+int rt_get_raw_counters(const rt_renderer *r, uint64_t *out, int n);
+int rt_diagnostic_build(void);
+
 /* Thread-local message for the last failing call. */
 const char *rt_last_error(void);
 /* Number of visible gfx950 devices (0 on a CPU-only host; never an error). */
