@@ -70,7 +70,9 @@ def main() -> int:
     ap.add_argument("--frames", type=int, default=None, help="spp per step (default: the config's)")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
-    ap.add_argument("--frames-per-launch", type=int, default=32)
+    ap.add_argument("--frames-per-launch", type=int, default=1024, help="tiles schedule: frames per launch")
+    ap.add_argument("--schedule", type=int, default=0, help="0 auto (queue), 1 tiles, 2 sample queue")
+    ap.add_argument("--job-frames", type=int, default=4, help="sample queue: frames per 8x8-tile job")
     ap.add_argument("--variant", type=int, default=0,
                     help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -115,7 +117,8 @@ def main() -> int:
         sd.frames = args.frames or sd.frames
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
-    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant)
+    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
+                 schedule=args.schedule, job_frames=args.job_frames)
     local_rows = r.local_rows
     max_rows = (sd.height + world - 1) // world
     part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)

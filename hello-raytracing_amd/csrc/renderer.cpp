@@ -20,6 +20,7 @@
 #include "rt_device.hpp"
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_queue(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 
 namespace {
 
@@ -41,6 +42,10 @@ template <typename T>
 struct DevBuf {
     T* ptr = nullptr;
     size_t cap = 0;  // elements
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
     void release() {
         if (ptr) (void)hipFree(ptr);
         ptr = nullptr;
@@ -97,7 +102,7 @@ struct rt_renderer {
     DevBuf<hrt_dev::SpherePair> sph_pairs;
     uint32_t n_spheres = 0;
     // culling BVH over the sphere slots (SCAN_BVH)
-    DevBuf<float4> bvh_nodes, bvh_sph;
+    DevBuf<float4> bvh_nodes, bvh4_nodes, bvh_sph;
     DevBuf<int> bvh_slot, bvh_large;
     hrt::SphereBvh bvh_host;
     DevBuf<float4> nodes;
@@ -105,6 +110,9 @@ struct rt_renderer {
     DevBuf<hrt_dev::MatDev> mats;
     uint32_t bvh_n = 0, bvh_m = 0;
     DevBuf<unsigned long long> counter;
+    DevBuf<float> samples;  // sample-queue colour buffer (frames x rows x W x 3)
+    DevBuf<unsigned long long> wave_trace;  // diagnostic build only
+    size_t wave_trace_words = 0;
 
     // host copy of the spheres (slot arrays are rebuilt when min_sphere_slots changes)
     std::vector<hrt::Sphere> spheres;
@@ -112,6 +120,7 @@ struct rt_renderer {
     rt_stats stats{};
     bool timing_pending = false;
     int last_variant = 0;
+    uint32_t last_schedule = 0;
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
@@ -176,11 +185,29 @@ int upload_spheres(rt_renderer* r) {
         o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
         o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
     }
+    // 4-wide nodes: 8 float4 each (minx, maxx, miny, maxy, minz, maxz, child words, unused)
+    std::vector<float4> bnodes4(8 * std::max<size_t>(B.nodes4.size(), 1));
+    for (size_t j = 0; j < B.nodes4.size(); j++) {
+        const hrt::SphereBvh4Node& n = B.nodes4[j];
+        float* o = &bnodes4[8 * j].x;
+        for (int c = 0; c < 4; c++) {
+            const bool used = n.child[c] != hrt::BVH4_EMPTY;
+            o[0 + c] = used ? rel_lo(n.minx[c], 0) : 0.0f;
+            o[4 + c] = used ? rel_hi(n.maxx[c], 0) : 0.0f;
+            o[8 + c] = used ? rel_lo(n.miny[c], 1) : 0.0f;
+            o[12 + c] = used ? rel_hi(n.maxy[c], 1) : 0.0f;
+            o[16 + c] = used ? rel_lo(n.minz[c], 2) : 0.0f;
+            o[20 + c] = used ? rel_hi(n.maxz[c], 2) : 0.0f;
+            o[24 + c] = __builtin_bit_cast(float, n.child[c]);
+            o[28 + c] = 0.0f;
+        }
+    }
     const size_t nleaf = B.slot.size();
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
     if (!rc) rc = ensure(r->sph_pairs, npairs);
     if (!rc) rc = ensure(r->bvh_nodes, bnodes.size());
+    if (!rc) rc = ensure(r->bvh4_nodes, bnodes4.size());
     if (!rc) rc = ensure(r->bvh_sph, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_slot, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_large, std::max<size_t>(B.large.size(), 1));
@@ -191,6 +218,8 @@ int upload_spheres(rt_renderer* r) {
         HIP_TRY(hipMemcpyAsync(r->sph_pairs.ptr, pairs.data(), npairs * sizeof(pairs[0]), hipMemcpyHostToDevice,
                                r->stream));
         HIP_TRY(hipMemcpyAsync(r->bvh_nodes.ptr, bnodes.data(), bnodes.size() * sizeof(float4),
+                               hipMemcpyHostToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->bvh4_nodes.ptr, bnodes4.data(), bnodes4.size() * sizeof(float4),
                                hipMemcpyHostToDevice, r->stream));
         if (nleaf) {
             HIP_TRY(hipMemcpyAsync(r->bvh_sph.ptr, B.sph.data(), nleaf * sizeof(float4), hipMemcpyHostToDevice,
@@ -208,6 +237,11 @@ int upload_spheres(rt_renderer* r) {
 }
 
 // variant 0 = the fastest exact scan for the scene: the culling BVH from 32 slots up, else the deferred scan.
+// schedule 0 = the sample queue (load-balanced at sample granularity).
+uint32_t resolve_schedule(const rt_renderer* r) {
+    return r->params.schedule ? r->params.schedule : RT_SCHEDULE_QUEUE;
+}
+
 int resolve_variant(const rt_renderer* r) {
     if (r->params.variant) return (int)r->params.variant;
     return r->n_spheres >= 32 ? hrt_dev::SCAN_BVH : hrt_dev::SCAN_DEFER;
@@ -258,6 +292,16 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.tris = r->tris.ptr;
     P.mats = r->mats.ptr;
     P.counter = r->counter.ptr;
+#ifdef HRT_STAMPS
+    {
+        const size_t words = 4ull * ((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u;
+        int rc2 = ensure(r->wave_trace, words);
+        if (rc2) return rc2;
+        HIP_TRY(hipMemsetAsync(r->wave_trace.ptr, 0, words * sizeof(unsigned long long), r->stream));
+        r->wave_trace_words = words;
+        P.wave_trace = r->wave_trace.ptr;
+    }
+#endif
     const hrt::SphereBvh& B = r->bvh_host;
     P.bvh_nodes = r->bvh_nodes.ptr;
     P.bvh_sph = r->bvh_sph.ptr;
@@ -265,6 +309,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.large_slots = r->bvh_large.ptr;
     P.nlarge = (uint32_t)B.large.size();
     P.bvh_root = B.root_word;
+    P.bvh4_nodes = r->bvh4_nodes.ptr;
+    P.bvh4_root = B.root4_word;
     for (int k = 0; k < 3; k++) P.bvh_rc[k] = B.root_center[k];
     P.bvh_rr = B.root_radius;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
@@ -279,17 +325,47 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     // the LDS copy of the BVH holds at most BVH_LDS_NODES nodes
     P.bvh_nnodes = (uint32_t)B.nodes.size();
     if (variant == hrt_dev::SCAN_BVH_LDS && P.bvh_nnodes > (uint32_t)hrt_dev::BVH_LDS_NODES) variant = hrt_dev::SCAN_BVH;
+    const uint32_t schedule = resolve_schedule(r);
+    if (schedule == RT_SCHEDULE_QUEUE && variant != hrt_dev::SCAN_SIMPLE && variant != hrt_dev::SCAN_DEFER)
+        variant = hrt_dev::SCAN_BVH;  // the queue kernels carry the simple, deferred and BVH scans
     r->last_variant = variant;
+    r->last_schedule = schedule;
 
-    const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
-    HIP_TRY(hipEventRecord(r->ev_start, r->stream));
     uint32_t launches = 0;
-    for (uint32_t done = 0; done < count; done += fpl) {
-        P.nframes = std::min(fpl, count - done);
-        P.time0 = time0 + done * dtime;
-        P.frame0 = r->frame_count + done;
-        HIP_TRY(hrt_launch_render(r->mode, variant, P, r->stream));
-        launches++;
+    if (schedule == RT_SCHEDULE_QUEUE) {
+        // frames per chunk: as many as the colour buffer budget holds
+        const size_t frame_floats = (size_t)P.nrows * r->width * 3u;
+        const size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
+        const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+        if (count) {
+            rc = ensure(r->samples, (size_t)chunk * frame_floats);
+            if (rc) return rc;
+        }
+        P.samples = r->samples.ptr;
+        P.queue = r->counter.ptr + 15;
+        P.tiles_w = (r->width + 7u) / 8u;
+        P.tiles_h = (P.nrows + 7u) / 8u;
+        HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+        for (uint32_t done = 0; done < count; done += chunk) {
+            P.nframes = std::min(chunk, count - done);
+            P.time0 = time0 + done * dtime;
+            P.frame0 = r->frame_count + done;
+            P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
+            P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * ((P.nframes + P.job_frames - 1u) / P.job_frames);
+            HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
+            HIP_TRY(hrt_launch_queue(r->mode, variant, P, r->stream));
+            launches += 2;
+        }
+    } else {
+        const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
+        HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+        for (uint32_t done = 0; done < count; done += fpl) {
+            P.nframes = std::min(fpl, count - done);
+            P.time0 = time0 + done * dtime;
+            P.frame0 = r->frame_count + done;
+            HIP_TRY(hrt_launch_render(r->mode, variant, P, r->stream));
+            launches++;
+        }
     }
     HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
     r->frame_count += count;  // end_frame, renderer.rs:409
@@ -315,6 +391,7 @@ int finish_stats(rt_renderer* r) {
     r->stats.node_tests = q[3];
     r->stats.tri_tests = q[4];
     r->stats.variant = (uint32_t)r->last_variant;
+    r->stats.schedule = r->last_schedule;
     r->timing_pending = false;
     return RT_OK;
 }
@@ -352,6 +429,9 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.row0 = 0;
     r->params.row_step = 1;
     r->params.frames_per_launch = 32;
+    r->params.schedule = RT_SCHEDULE_AUTO;
+    r->params.queue_budget_mb = 4096;
+    r->params.job_frames = 4;
     if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
         rt_destroy(r);
@@ -393,7 +473,8 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
-    if (p->variant > 8) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->variant > 10) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->schedule > RT_SCHEDULE_QUEUE) return fail(RT_ERR_ARG, "rt_set_params: unknown schedule");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;
@@ -550,6 +631,13 @@ int rt_get_raw_counters(const rt_renderer* r, uint64_t* out, int n) {
     int rc = finish_stats(const_cast<rt_renderer*>(r));
     if (rc) return rc;
     for (int i = 0; i < n; i++) out[i] = i < RT_RAW_COUNTERS ? r->raw_counters[i] : 0;
+    return RT_OK;
+}
+
+int rt_get_wave_trace(rt_renderer* r, uint64_t* out, size_t n_words) {
+    if (!r || !out) return fail(RT_ERR_ARG, "rt_get_wave_trace: null");
+    if (n_words > r->wave_trace_words) return fail(RT_ERR_ARG, "rt_get_wave_trace: more words than recorded");
+    if (n_words) HIP_TRY(hipMemcpy(out, r->wave_trace.ptr, n_words * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -64,8 +64,14 @@ constexpr int BVH_LDS_NODES = 320;  // node capacity of the LDS copy (20 KB)
 constexpr int BVH_STACK_LDS = 12;   // stack entries per lane for variant 7 (overflow -> exact full scan)
 constexpr int SCAN_BVH_CULL = 8;    // variant 4 + popped subtrees re-culled against the current best t
 constexpr int BVH_STACK_CULL = 12;  // (node word, entry distance) pairs per lane for variant 8
+constexpr int SCAN_BVH4 = 9;         // the culling tree collapsed to 4-wide nodes, sorted child order
+constexpr int SCAN_BVH4_CULL = 10;   // variant 9 + popped subtrees re-culled against the current best t
 constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
-constexpr int BVH_STACK = 24;   // traversal stack entries per lane (LDS); overflow -> exact full scan
+constexpr uint32_t BVH4_EMPTY = 0x80000000u;  // unused child slot (empty leaf)
+#ifndef HRT_BVH_STACK
+#define HRT_BVH_STACK 24
+#endif
+constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (LDS); overflow -> exact full scan
 
 // Kernel arguments (passed by value in the kernarg segment).
 struct KParams {
@@ -91,12 +97,21 @@ struct KParams {
     const int* large_slots;       // slots scanned linearly for every ray
     uint32_t nlarge, bvh_root;    // large-list length, root child word
     uint32_t bvh_nnodes;          // internal nodes (4 float4 each)
+    const float4* bvh4_nodes;     // the same tree collapsed 4-wide: 8 float4 per node (SphereBvh4Node)
+    uint32_t bvh4_root, pad_w;    // root child word of the 4-wide tree
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     const float4* nodes;          // 2 float4 per node: min, max
     const TriDev* tris;
     const MatDev* mats;
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
+    unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
+    // sample-queue schedule (k_trace / k_accumulate)
+    float* samples;               // nframes x nrows x W x 3 sample colours, frame-major
+    unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
+    unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
+    uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
+    uint32_t job_frames, pad_j;   // frames per job (a job = one tile x job_frames frames)
 };
 
 struct f3 {

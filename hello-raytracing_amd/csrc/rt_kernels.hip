@@ -17,6 +17,8 @@
 //     traversal order and 600-step cap.
 #include "rt_device.hpp"
 
+#include <algorithm>
+
 using namespace hrt_dev;
 
 namespace {
@@ -32,6 +34,14 @@ __device__ __forceinline__ unsigned long long hrt_stamp() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+// Constant 100 MHz clock (s_memrealtime), to calibrate s_memtime and measure wave residency.
+__device__ __forceinline__ unsigned long long hrt_realtime() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
@@ -360,6 +370,127 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     return bi;
 }
 
+// Compare-exchange of (entry distance, child word) pairs into ascending distance.
+__device__ __forceinline__ void cx_pair(float& ta, uint32_t& wa, float& tb, uint32_t& wb) {
+    const bool sw = tb < ta;
+    const float t0 = sw ? tb : ta, t1 = sw ? ta : tb;
+    const uint32_t w0 = sw ? wb : wa, w1 = sw ? wa : wb;
+    ta = t0; tb = t1; wa = w0; wb = w1;
+}
+
+// Variants 9/10: the culling tree collapsed to 4-wide nodes (host/sphere_bvh.cpp Collapser). One
+// iteration tests the four child boxes of a node (SoA loads, the same padded slab test and boxes as
+// variant 4), sorts the hit children by entry distance, continues into the nearest and pushes the rest
+// farthest-first. Same exactness argument as scan_spheres_bvh; only the visiting order differs, and the
+// (t, slot) lexicographic minimum is order-independent.
+template <int STACK_CAP, bool CULL_POP>
+__device__ __forceinline__ int scan_spheres_bvh4(const KParams& P, const Ray& r, float& best, uint32_t* stack,
+                                                 Tally& tally) {
+    const float a = dot(r.d, r.d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
+    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    float bt = best;
+    int bi = -1;
+    for (uint32_t k = 0; k < P.nlarge; k++) {
+        const int i = P.large_slots[k];
+        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
+        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+    }
+    tally.spheres += P.nlarge;
+
+    const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
+    const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
+    const float D = dl * 1.001f + P.bvh_rr;
+    const float dn = __builtin_amdgcn_sqrtf(a);
+    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
+    const float pad = 2.02f * delta;
+    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+    const float4* __restrict__ nodes = P.bvh4_nodes;
+
+    uint32_t node = P.bvh4_root;
+    int sp = 0;
+    bool overflow = false;
+    while (true) {
+        if (!(node & BVH_LEAF_BIT)) {
+            const float4* nd = nodes + 8u * node;
+            const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5];
+            const float4 cw = nd[6];
+            float t[4];
+            uint32_t w[4];
+            const float mnxa[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, mxxa[4] = {mxx.x, mxx.y, mxx.z, mxx.w};
+            const float mnya[4] = {mny.x, mny.y, mny.z, mny.w}, mxya[4] = {mxy.x, mxy.y, mxy.z, mxy.w};
+            const float mnza[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, mxza[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+            const float cwa[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                float te;
+                const bool h = padded_box_hit(make_float4(mnxa[c], mnya[c], mnza[c], 0.0f),
+                                              make_float4(mxxa[c], mxya[c], mxza[c], 0.0f), lo, hi, inv, bt, te);
+                w[c] = __float_as_uint(cwa[c]);
+                t[c] = (h && w[c] != BVH4_EMPTY) ? te : __builtin_inff();
+                tally.boxes += w[c] != BVH4_EMPTY;
+            }
+            cx_pair(t[0], w[0], t[1], w[1]);
+            cx_pair(t[2], w[2], t[3], w[3]);
+            cx_pair(t[0], w[0], t[2], w[2]);
+            cx_pair(t[1], w[1], t[3], w[3]);
+            cx_pair(t[1], w[1], t[2], w[2]);
+            if (t[0] != __builtin_inff()) {
+#pragma unroll
+                for (int c = 3; c >= 1; c--) {
+                    if (t[c] != __builtin_inff()) {
+                        if (sp < STACK_CAP) {
+                            stack[sp * 256] = w[c];
+                            if constexpr (CULL_POP) stack[(STACK_CAP + sp) * 256] = __float_as_uint(t[c]);
+                            sp++;
+                        } else {
+                            overflow = true;
+                        }
+                    }
+                }
+                node = w[0];
+                continue;
+            }
+        } else {
+            const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+            for (uint32_t j = 0; j < cnt; j++) {
+                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
+                const int i = P.bvh_slot[first + j];
+                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+            }
+            tally.spheres += cnt;
+        }
+        if constexpr (CULL_POP) {
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                if (__uint_as_float(stack[(STACK_CAP + sp) * 256]) <= bt) {
+                    node = stack[sp * 256];
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+        } else {
+            if (sp == 0) break;
+            node = stack[(--sp) * 256];
+        }
+    }
+    if (overflow) {
+        tally.spheres += P.nslots;
+        return scan_spheres(P, r, best);
+    }
+    best = bt;
+    return bi;
+}
+
 // Variant 5: the same culling BVH and exactness argument as scan_spheres_bvh, traversed "while-while"
 // (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps walking internal nodes until every
 // lane of the wave holds a leaf (or has nothing left), then the wave tests leaves together. This keeps the
@@ -545,6 +676,10 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
             bi = scan_spheres_bvh<BVH_STACK_LDS>(P, r, best, (uint32_t*)lds, tally, lds_nodes);
         } else if constexpr (SCAN == SCAN_BVH_CULL) {
             bi = scan_spheres_bvh<BVH_STACK_CULL, true>(P, r, best, (uint32_t*)lds, tally, P.bvh_nodes);
+        } else if constexpr (SCAN == SCAN_BVH4) {
+            bi = scan_spheres_bvh4<BVH_STACK, false>(P, r, best, (uint32_t*)lds, tally);
+        } else if constexpr (SCAN == SCAN_BVH4_CULL) {
+            bi = scan_spheres_bvh4<BVH_STACK_CULL, true>(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_DEFER) {
             bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
             tally.spheres += P.nslots;
@@ -649,18 +784,23 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 }  // namespace
 
 // One launch = P.nframes frames over this renderer's rows. Grid: (ceil(W/16), ceil(nrows/16)).
+#ifdef HRT_WAVES_PER_EU
+#define HRT_OCC __attribute__((amdgpu_waves_per_eu(HRT_WAVES_PER_EU)))
+#else
+#define HRT_OCC
+#endif
 template <int MODE, int SCAN>
-__global__ __launch_bounds__(256) void k_render(const KParams P) {
+__global__ __launch_bounds__(256) HRT_OCC void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* lds_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
-    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVH_WW) {
+    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVH_WW || SCAN == SCAN_BVH4) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
         lds_list = bvh_stack + threadIdx.x;
     }
-    if constexpr (SCAN == SCAN_BVH_CULL) {
+    if constexpr (SCAN == SCAN_BVH_CULL || SCAN == SCAN_BVH4_CULL) {
         __shared__ uint32_t bvh_stack_c[2 * BVH_STACK_CULL * 256];
         lds_list = bvh_stack_c + threadIdx.x;
     }
@@ -701,8 +841,9 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     }
 
 #ifdef HRT_STAMPS  // diagnostic build only (lib/libhrt_diag.so): wave cycles per region
-    unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb, st_tc;
+    unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb = 0, st_tc;
     const unsigned long long st_start = hrt_stamp();
+    const unsigned long long rt_start = hrt_realtime();
 #endif
     while (f < P.nframes) {
         bool done = true;
@@ -758,11 +899,39 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
         px[2] = acc2;
     }
 #ifdef HRT_STAMPS
-    if (lane == 0) {
-        atomicAdd(P.counter + 8, st_trav);
-        atomicAdd(P.counter + 9, st_shade);
-        atomicAdd(P.counter + 10, st_gen);
-        atomicAdd(P.counter + 11, hrt_stamp() - st_start);
+    // Loop-carried sums are per lane (a lane stops adding once its frames are done), so summed over the
+    // lanes they give lane-cycles per region; the lifetime is counted per lane too (x64), and the
+    // remainder is lane-cycles spent idle behind the wave's slowest lane.
+    {
+        unsigned long long life = valid ? hrt_stamp() - st_start : 0ull;
+        unsigned long long v[5] = {st_trav, st_shade, st_gen, life, queries};
+        if (!valid) v[0] = v[1] = v[2] = 0ull;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
+        }
+        if (lane == 0) {
+            for (int c = 0; c < 4; c++) atomicAdd(P.counter + 8 + c, v[c]);
+            // wave residency in 100 MHz ticks, wave count, and the memtime ticks of the same interval
+            const unsigned long long t1 = hrt_stamp(), r1 = hrt_realtime();
+            atomicAdd(P.counter + 12, r1 - rt_start);
+            atomicAdd(P.counter + 13, 1ull);
+            atomicAdd(P.counter + 14, t1 - st_start);
+            if (P.wave_trace) {
+                // one record per wave of the FIRST launch of the draw (frame0 == trace frame): start/end in
+                // 100 MHz ticks, HW_ID | XCC_ID << 32, queries of lane 0's pixel
+                unsigned hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                const size_t wid = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4u + wave;
+                unsigned long long* rec = P.wave_trace + 4u * wid;
+                rec[0] = rt_start;
+                rec[1] = r1;
+                rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+                rec[3] = v[4];
+            }
+        }
     }
 #endif
     // One atomic per wave and counter: rays, box tests, sphere tests, tri-program node and triangle tests.
@@ -964,6 +1133,192 @@ __global__ __launch_bounds__(256) void k_render_lanes(const KParams P) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Sample-queue schedule (rt_params.schedule = RT_SCHEDULE_QUEUE). The tiles schedule (k_render) gives
+// every lane one pixel for all frames of a launch, so a pixel whose paths are long (glass, crevices:
+// 20+ queries per sample) serialises its whole frame chunk on one lane and the launch waits for it
+// (wave records: one C4 wave ran 128 ms of a 129 ms launch while the GPU averaged < 1 resident wave
+// per SIMD), and a workgroup's slots stay taken until its slowest wave ends.
+// Here a persistent grid (resident capacity) pulls JOBS from a global counter: a job is one 8x8 tile
+// and `job_frames` frames, i.e. 64 x job_frames samples. A wave hands the samples of its current job
+// to its lanes as they become free (wave-uniform bookkeeping, no per-sample atomics), and takes the
+// next job as soon as the current one has no samples left, while older samples are still in flight.
+// Lanes therefore never idle until the queue is empty, a wave's lanes stay inside one tile (ray
+// coherence: an incoherent sample queue measured 2.65x slower on C3), and one tile's frames are
+// spread over many waves. Each sample's colour goes to a frame-major buffer; k_accumulate then folds
+// the colours into the image in frame order per pixel with the reference's mix
+// (shader_sphere.wgsl:264-271), so the image is bit-identical to k_render's and to count x rt_draw.
+template <int MODE, int SCAN>
+__global__ __launch_bounds__(256) void k_trace(const KParams P) {
+    const uint32_t lane = threadIdx.x & 63u;
+    void* lds_list = nullptr;
+    if constexpr (SCAN == SCAN_DEFER) {
+        __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
+        lds_list = cand + threadIdx.x;
+    } else if constexpr (SCAN == SCAN_BVH) {
+        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+        lds_list = bvh_stack + threadIdx.x;
+    }
+    Tally tally;
+    uint32_t queries = 0;
+    const uint32_t ntiles = P.tiles_w * P.tiles_h;
+    const unsigned long long below = (1ull << lane) - 1ull;
+
+    // wave-uniform job state
+    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    bool drained = false;
+    // lane state
+    Ray ray;
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    float sky_t = 0.0f;
+    uint32_t s = 0, bounce = 0, x = 0, kr = 0, fl = 0;
+    bool have = false;
+    while (true) {
+        // refill: free lanes take the next samples of the wave's job, fetching jobs as they run out
+        bool need = !have && !drained;
+        unsigned long long m = __ballot(need);
+        while (m != 0ull) {
+            if (job_next == job_total) {
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                j = __shfl(j, 0);
+                if (j >= P.njobs) {
+                    drained = true;
+                    break;
+                }
+                const uint32_t chunk = (uint32_t)(j / ntiles);
+                job_tile = (uint32_t)(j % ntiles);
+                job_f0 = chunk * P.job_frames;
+                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
+                job_next = 0;
+            }
+            const uint32_t avail = job_total - job_next;
+            const uint32_t rank = (uint32_t)__popcll(m & below);
+            if (need && rank < avail) {
+                const uint32_t sid = job_next + rank;
+                const uint32_t l = sid & 63u;
+                fl = job_f0 + (sid >> 6);
+                x = (job_tile % P.tiles_w) * 8u + (l & 7u);
+                kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
+                need = false;
+                if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
+                    const uint32_t y = P.row0 + kr * P.row_step;
+                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
+                    sky_t = ray.d.y * 0.5f + 0.5f;
+                    att = mk(1.0f, 1.0f, 1.0f);
+                    bounce = 0;
+                    have = true;
+                }
+            }
+            const uint32_t took = min((uint32_t)__popcll(m), avail);
+            job_next += took;
+            m = __ballot(need);
+        }
+        if (drained && __ballot(have) == 0ull) break;
+        if (!have) continue;
+        bool done = true;
+        if (bounce < P.bounces) {
+            Hit h;
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, nullptr);
+            queries++;
+            if (hit) {
+                scatter<MODE>(s, ray, h);
+                att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                bounce++;
+                done = bounce >= P.bounces;
+            }
+        }
+        if (done) {
+            // trace() epilogue (:241-242): the sample colour, folded in by k_accumulate
+            const float u = 1.0f - sky_t;
+            const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+            const f3 c = att * sky;
+            float* o = P.samples + ((size_t)fl * P.nrows * P.W + (size_t)kr * P.W + x) * 3u;
+            o[0] = c.x;
+            o[1] = c.y;
+            o[2] = c.z;
+            have = false;
+        }
+    }
+    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+    }
+}
+
+// Folds P.nframes sample colours per pixel into the image, in frame order, with the same expression
+// k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per pixel; frame-major reads are
+// coalesced across the wave.
+__global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
+    const size_t npx = (size_t)P.nrows * P.W;
+    const size_t p = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= npx) return;
+    float* px = P.image + p * 3u;
+    float acc0 = px[0], acc1 = px[1], acc2 = px[2];
+    const float* c = P.samples + p * 3u;
+    for (uint32_t f = 0; f < P.nframes; f++, c += npx * 3u) {
+        const float fc = (float)(P.frame0 + f);
+        const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
+        const float omw = 1.0f - w;
+        acc0 = acc0 * omw + (0.0f + c[0]) * w;
+        acc1 = acc1 * omw + (0.0f + c[1]) * w;
+        acc2 = acc2 * omw + (0.0f + c[2]) * w;
+    }
+    px[0] = acc0;
+    px[1] = acc1;
+    px[2] = acc2;
+}
+
+template <typename K>
+static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stream) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+    }
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+    if (e != hipSuccess) return e;
+    const unsigned long long want = (P.njobs + 3ull) / 4ull;  // no more waves than jobs
+    const unsigned long long cap = (unsigned long long)std::max(1, per_cu) * (unsigned long long)cus;
+    const dim3 grid((unsigned)std::min(want, cap));
+    hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, P);
+    return hipGetLastError();
+}
+
+// Sample-queue launch pair: trace every sample of the chunk, then fold them into the image.
+// variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (others are resolved to SCAN_BVH by the host).
+hipError_t hrt_launch_queue(int mode, int variant, const KParams& P, hipStream_t stream) {
+    if (P.njobs == 0) return hipSuccess;
+    hipError_t e;
+    switch (mode) {
+    case MODE_SPHERE:
+        if (variant == SCAN_SIMPLE) e = launch_persistent(k_trace<MODE_SPHERE, SCAN_SIMPLE>, P, stream);
+        else if (variant == SCAN_DEFER) e = launch_persistent(k_trace<MODE_SPHERE, SCAN_DEFER>, P, stream);
+        else e = launch_persistent(k_trace<MODE_SPHERE, SCAN_BVH>, P, stream);
+        break;
+    case MODE_TRIS: e = launch_persistent(k_trace<MODE_TRIS, SCAN_SIMPLE>, P, stream); break;
+    default:
+        if (variant == SCAN_SIMPLE) e = launch_persistent(k_trace<MODE_MIXED, SCAN_SIMPLE>, P, stream);
+        else if (variant == SCAN_DEFER) e = launch_persistent(k_trace<MODE_MIXED, SCAN_DEFER>, P, stream);
+        else e = launch_persistent(k_trace<MODE_MIXED, SCAN_BVH>, P, stream);
+        break;
+    }
+    if (e != hipSuccess) return e;
+    const size_t npx = (size_t)P.nrows * P.W;
+    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npx + 255u) / 256u)), dim3(256), 0, stream, P);
+    return hipGetLastError();
+}
+
 // Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI). variant: SCAN_* (0 = default).
 hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_t stream) {
     dim3 block(256);
@@ -979,6 +1334,8 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         else if (variant == SCAN_LANES) hipLaunchKernelGGL(k_render_lanes, grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_LDS>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_CULL>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH4) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH4>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH4_CULL) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH4_CULL>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
@@ -989,6 +1346,8 @@ hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_
         else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_WW>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_LDS>), grid, block, 0, stream, P);
         else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_CULL>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH4) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH4>), grid, block, 0, stream, P);
+        else if (variant == SCAN_BVH4_CULL) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH4_CULL>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
         break;
     }

@@ -25,6 +25,7 @@ RT_ERR_COMPARE = -6
 RT_MODE_SPHERE = 0
 RT_MODE_TRIS = 1
 RT_MODE_MIXED = 2
+RT_SCHEDULE_AUTO, RT_SCHEDULE_TILES, RT_SCHEDULE_QUEUE = 0, 1, 2
 
 
 class RtParams(C.Structure):
@@ -36,6 +37,9 @@ class RtParams(C.Structure):
         ("row_step", C.c_uint32),
         ("frames_per_launch", C.c_uint32),
         ("variant", C.c_uint32),
+        ("schedule", C.c_uint32),
+        ("queue_budget_mb", C.c_uint32),
+        ("job_frames", C.c_uint32),
     ]
 
 
@@ -49,7 +53,7 @@ class RtStats(C.Structure):
         ("box_tests", C.c_uint64),
         ("sphere_tests", C.c_uint64),
         ("variant", C.c_uint32),
-        ("pad0", C.c_uint32),
+        ("schedule", C.c_uint32),
         ("node_tests", C.c_uint64),
         ("tri_tests", C.c_uint64),
     ]
@@ -82,6 +86,7 @@ SIGNATURES = {
     "rt_get_stats": (C.c_int, [_P, C.POINTER(RtStats)]),
     "rt_get_raw_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "rt_diagnostic_build": (C.c_int, []),
+    "rt_get_wave_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_last_error": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),
     "rt_build_info": (C.c_char_p, []),

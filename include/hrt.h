@@ -62,8 +62,21 @@ typedef struct rt_params {
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
     uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots up, else 3), 1 simple,
                                   2 packed + interval filter, 3 packed + deferred exact candidates,
-                                  4 conservative culling BVH; all bit-identical   */
+                                  4 conservative culling BVH, 5 BVH while-while, 6 BVH lane state
+                                  machine, 7 BVH nodes in LDS, 8 BVH + pop re-culling, 9 the BVH
+                                  collapsed 4-wide, 10 4-wide + pop re-culling; all bit-identical
+                                                                                   */
+    uint32_t schedule;         /* work schedule of rt_draw_frames: 0 auto, 1 tiles (one lane per pixel
+                                  for a launch's frames, in-register accumulation), 2 sample queue
+                                  (persistent grid pulling (pixel, frame) samples + in-order fold);
+                                  bit-identical                               */
+    uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
+    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 4        */
 } rt_params;
+
+#define RT_SCHEDULE_AUTO 0u
+#define RT_SCHEDULE_TILES 1u
+#define RT_SCHEDULE_QUEUE 2u
 
 typedef struct rt_stats {
     uint64_t queries;      /* closest-hit queries (rays) traced by the last draw call                  */
@@ -73,8 +86,8 @@ typedef struct rt_stats {
     uint32_t local_rows;   /* rows owned by this renderer                                              */
     uint64_t box_tests;    /* padded-box tests of the sphere culling BVH (variant 4), last draw call    */
     uint64_t sphere_tests; /* ray-sphere tests (slots scanned, or BVH leaf + large-list tests)          */
-    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..5)                         */
-    uint32_t pad0;
+    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..10)                        */
+    uint32_t schedule;     /* schedule the last draw call ran (RT_SCHEDULE_TILES / _QUEUE)             */
     uint64_t node_tests;   /* triangle program: implicit-heap node (slab) tests                         */
     uint64_t tri_tests;    /* triangle program: Moller-Trumbore tests                                   */
 } rt_stats;
@@ -129,6 +142,10 @@ int rt_get_stats(const rt_renderer *r, rt_stats *out);
 #define RT_RAW_COUNTERS 16
 int rt_get_raw_counters(const rt_renderer *r, uint64_t *out, int n);
 int rt_diagnostic_build(void);
+/* Diagnostic build: per-wave records of the last launch of the last draw, 4 words per wave in
+ * (blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave order: start and end (100 MHz ticks), HW_ID |
+ * XCC_ID << 32, closest-hit queries of the wave. Zero words in the product build. */
+int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 
 /* Thread-local message for the last failing call. */
 const char *rt_last_error(void);

@@ -68,11 +68,67 @@ def test_golden_scene_hip_vs_oracle_and_golden(name):
 def test_draw_frames_equals_per_frame_draws():
     sd = scenes.golden_scene("complex_scene", 96, 64)
     a = render_reference_protocol(sd, 12).renderer.read_image()
-    r = scenes.make_renderer(sd)
-    r.set_params(frames_per_launch=5)  # 3 launches: 5 + 5 + 2
-    r.draw_frames(12, 1000, 10)
-    assert r.frame_count == 12
-    np.testing.assert_array_equal(r.read_image().view(np.uint32), a.view(np.uint32))
+    for schedule in (hrt.RT_SCHEDULE_TILES, hrt.RT_SCHEDULE_QUEUE):
+        r = scenes.make_renderer(sd)
+        r.set_params(frames_per_launch=5, schedule=schedule)  # tiles: 3 launches, 5 + 5 + 2
+        r.draw_frames(12, 1000, 10)
+        assert r.frame_count == 12 and r.stats().schedule == schedule
+        np.testing.assert_array_equal(r.read_image().view(np.uint32), a.view(np.uint32))
+
+
+def _schedule_cases():
+    c3 = scenes.config_c3(90, 53, 5)  # W, H not multiples of the 8x8 tile
+    c4 = scenes.config_c4(72, 41, 3)
+    golden = scenes.golden_scene("dielectric_materials", 64, 40)
+    golden.frames = 6
+    return [c3, c4, golden]
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_sample_queue_equals_tiles(case):
+    """The sample-queue schedule (persistent k_trace + in-order k_accumulate) gives the tiles schedule's
+    bits and exact work counters, for sphere, mixed and partitioned renders."""
+    sd = _schedule_cases()[case]
+    for row0, step in [(0, 1), (1, 3)]:
+        out = []
+        for schedule in (hrt.RT_SCHEDULE_TILES, hrt.RT_SCHEDULE_QUEUE):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=schedule, row0=row0, row_step=step, job_frames=3)  # ragged last job
+            r.set_frame_count(3)
+            r.draw_frames(sd.frames, 2000, 7)
+            out.append((r.read_image(), r.stats()))
+        (a, sa), (b, sb) = out
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert (sa.queries, sa.box_tests, sa.sphere_tests, sa.node_tests, sa.tri_tests) == \
+               (sb.queries, sb.box_tests, sb.sphere_tests, sb.node_tests, sb.tri_tests)
+        assert sb.schedule == hrt.RT_SCHEDULE_QUEUE and sb.samples == sa.samples
+
+
+def test_sample_queue_chunks_and_tris_mode():
+    """Frame chunks bounded by the colour-buffer budget (1 and 2 frames per chunk at 320x240) and the
+    triangle program under the queue schedule."""
+    sd = scenes.golden_scene("metal_materials", 320, 240)
+    ref = scenes.make_renderer(sd)
+    ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
+    ref.draw_frames(5, 1000, 10)
+    for mb in (1, 2):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb)
+        r.draw_frames(5, 1000, 10)
+        assert r.stats().launches == 2 * ((5 + mb - 1) // mb)
+        np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
+    scene = hrt.SceneTris.new_suzane(96, 72)
+    scene.init()
+    sd = scenes.SceneDef("suzane", hrt.RT_MODE_TRIS, 96, 72, scene.camera, bvh=scene.tris_bvh.view(), frames=4)
+    imgs = []
+    for schedule in (hrt.RT_SCHEDULE_TILES, hrt.RT_SCHEDULE_QUEUE):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=schedule)
+        r.draw_frames(4, 1000, 10)
+        imgs.append(r.read_image())
+    np.testing.assert_array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
+    ref_img, _ = scenes.oracle_render(sd)
+    assert_parity(imgs[1], ref_img, "suzane tris, queue schedule")
 
 
 def test_query_count_matches_oracle():
@@ -154,14 +210,14 @@ def test_rtiow_cover_scene_small():
     assert r.stats().queries == q
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_scan_variants_bit_identical(variant):
     """Every sphere-scan kernel variant gives the same bits (and ray counts) as the oracle."""
     for sd in (scenes.config_c3(192, 108, 4), scenes.golden_scene("dielectric_materials", 128, 128),
                scenes.golden_scene("complex_scene", 128, 128)):
         sd.frames = 4
         r = scenes.make_renderer(sd)
-        r.set_params(variant=variant)
+        r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
         ref, q = scenes.oracle_render(sd)
         assert_parity(r.read_image(), ref, f"{sd.name} variant {variant}")
@@ -172,9 +228,9 @@ def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
     imgs = []
-    for variant in (1, 2, 3, 4, 5, 6, 7, 8):
+    for variant in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
         r = scenes.make_renderer(sd)
-        r.set_params(variant=variant)
+        r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
         imgs.append((r.read_image(), r.stats().queries))
     for img, q in imgs[1:]:
@@ -216,12 +272,12 @@ def _random_scene(kind: str, seed: int):
 def test_culling_bvh_exact_on_adversarial_scenes(kind):
     sd = _random_scene(kind, 7)
     out = []
-    for variant in (1, 4, 5, 6, 7, 8):
+    for variant in (1, 4, 5, 6, 7, 8, 9, 10):
         r = scenes.make_renderer(sd)
-        r.set_params(variant=variant)
+        r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
         out.append((r.read_image(), r.stats()))
-    for (img, st), v in zip(out[1:], (4, 5, 6, 7, 8)):
+    for (img, st), v in zip(out[1:], (4, 5, 6, 7, 8, 9, 10)):
         np.testing.assert_array_equal(out[0][0].view(np.uint32), img.view(np.uint32))
         assert out[0][1].queries == st.queries
         assert st.variant == v and st.sphere_tests < out[0][1].sphere_tests
@@ -234,9 +290,9 @@ def test_culling_bvh_with_zero_radius_slots():
     sd = scenes.golden_scene("complex_scene", 96, 64)
     sd.frames = 6
     out = []
-    for variant in (1, 4, 5, 6, 7, 8):
+    for variant in (1, 4, 5, 6, 7, 8, 9, 10):
         r = scenes.make_renderer(sd)  # 25 spheres + 75 zero slots = 100 slots
-        r.set_params(variant=variant)
+        r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
         out.append(r.read_image())
     for img in out[1:]:
