@@ -37,8 +37,21 @@ def test_library_exports_every_declared_symbol():
         assert getattr(L, n) is not None
 
 
+def _header_struct(name):
+    """(type, field) pairs of `typedef struct name {...} name;` in include/hrt.h (comments stripped)."""
+    text = (ROOT / "include" / "hrt.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), text, flags=re.S).group(1)
+    return [(t, n.strip()) for t, names in re.findall(r"(uint32_t|uint64_t|double)\s+([\w\s,]+);", body)
+            for n in names.split(",")]
+
+
 def test_struct_layouts_match_header():
-    assert C.sizeof(hrt.RtParams) == 7 * 4
+    ctypes_of = {"uint32_t": C.c_uint32, "uint64_t": C.c_uint64, "double": C.c_double}
+    for py, name in ((hrt.RtParams, "rt_params"), (hrt.RtStats, "rt_stats")):
+        fields = _header_struct(name)
+        assert [(f, ctypes_of[t]) for t, f in fields] == list(py._fields_), name
+    assert C.sizeof(hrt.RtParams) == 10 * 4
     assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
