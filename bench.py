@@ -60,6 +60,9 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
     }
 
 
+MODE_NAMES = {0: "sphere", 1: "tris", 2: "mixed"}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,7 +75,7 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--frames-per-launch", type=int, default=1024, help="tiles schedule: frames per launch")
     ap.add_argument("--schedule", type=int, default=0, help="0 auto (queue), 1 tiles, 2 sample queue")
-    ap.add_argument("--job-frames", type=int, default=4, help="sample queue: frames per 8x8-tile job")
+    ap.add_argument("--job-frames", type=int, default=8, help="sample queue: frames per 8x8-tile job")
     ap.add_argument("--variant", type=int, default=0,
                     help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -156,6 +159,9 @@ def main() -> int:
     node_tests = 0
     tri_tests = 0
     variant = 0
+    schedule = 0
+    trace_ms = 0.0
+    trace_launches = 0
     for i in range(args.steps):
         st = step()
         queries += st.queries
@@ -166,13 +172,17 @@ def main() -> int:
         node_tests += st.node_tests
         tri_tests += st.tri_tests
         variant = st.variant
-        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernel {st.kernel_ms:.1f} ms, "
+        schedule = st.schedule
+        trace_ms += st.trace_ms
+        trace_launches += st.trace_launches
+        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernels {st.kernel_ms:.1f} ms (trace {st.trace_ms:.1f}), "
             f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
     barrier()
     elapsed = time.perf_counter() - t0
 
-    stats_t = torch.tensor([elapsed, float(queries), kernel_ms, float(launches), float(box_tests),
-                            float(sphere_tests), float(node_tests), float(tri_tests)], dtype=torch.float64,
+    stats_t = torch.tensor([elapsed, float(queries), trace_ms, float(trace_launches), float(box_tests),
+                            float(sphere_tests), float(node_tests), float(tri_tests), kernel_ms],
+                           dtype=torch.float64,
                            device=dev if args.backend == "nccl" else "cpu")
     if dist is not None:
         all_t = [torch.zeros_like(stats_t) for _ in range(world)]
@@ -185,7 +195,8 @@ def main() -> int:
 
     if rank == 0:
         value = total_q / t_max / 1e6
-        # roofline of the render kernel on rank 0: algorithmic FLOPs per launch / HIP-event launch time.
+        # roofline of the ray-tracing kernel (k_trace under the sample queue, k_render under tiles) on
+        # rank 0: algorithmic FLOPs per launch / its HIP-event launch time (events around each launch).
         # Algorithmic = SURVEY 8(d)'s per-ray figure (18 FLOP per slot + ~90 for hit record and scatter)
         # x rays. executed = the tests the kernel actually ran (exact counters): 18 per ray-sphere test,
         # 12 per padded box test — with the culling BVH the two differ by ~30x.
@@ -201,7 +212,10 @@ def main() -> int:
         executed = ((SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q + tri_flop)
                     / nl / (avg_launch_ms * 1e-3) / 1e12)
         px = local_rows * sd.width
-        alg_bytes = 24.0 * px + 64.0 * nslots  # framebuffer read+write per launch + sphere arrays
+        if schedule == 2:  # k_trace writes one 12 B colour per sample; the sphere arrays are read once
+            alg_bytes = 12.0 * px * sd.frames * args.steps / nl + 64.0 * nslots
+        else:  # k_render reads and writes the framebuffer once per launch
+            alg_bytes = 24.0 * px + 64.0 * nslots
         traffic = None
         pmc = ROOT / "profiles" / "pmc_summary.json"
         if pmc.exists():
@@ -241,7 +255,10 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": f"k_render<sphere, scan variant {variant}>",
+                "kernel": (f"k_trace<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if schedule == 2
+                           else f"k_render<{MODE_NAMES[sd.mode]}, scan variant {variant}>"),
+                "schedule": {1: "tiles", 2: "sample-queue"}.get(schedule, str(schedule)),
+                "all_kernels_ms_per_step": round(float(all_t[0, 8]) / args.steps, 3),
                 "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),
                 "box_tests_per_ray": round(my_box / max(my_q, 1.0), 3),
                 "tri_node_tests_per_ray": round(my_nodes / max(my_q, 1.0), 3),
@@ -261,7 +278,8 @@ def main() -> int:
         if args.verify:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)
-            ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant)
+            ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
+                             job_frames=args.job_frames)
             ref_r.draw_frames(sd.frames, 1000, 10)
             ref_img = torch.from_numpy(ref_r.read_image())
             same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 
 namespace hrt {
@@ -46,6 +47,10 @@ struct Builder {
     std::vector<Prim> prims;
     SphereBvh* out;
     uint32_t max_depth = 0;
+    // leaf policy (HRT_BVH_MAX_LEAF / HRT_BVH_LEAF_DEPTH / HRT_BVH_TRAVERSAL_COST override, for tuning)
+    uint32_t max_leaf = BVH_MAX_LEAF;
+    uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
+    double traversal_cost = 0.5;
 
     uint32_t leaf_word(size_t first, size_t count) {
         uint32_t f = (uint32_t)out->slot.size();
@@ -63,7 +68,7 @@ struct Builder {
         for (size_t i = first; i < first + count; i++) b.grow(prims[i].box);
         *bounds = b;
         max_depth = std::max(max_depth, depth);
-        if (count <= 1 || (count <= BVH_MAX_LEAF && depth >= 8)) return leaf_word(first, count);
+        if (count <= 1 || (count <= max_leaf && depth >= leaf_depth)) return leaf_word(first, count);
 
         // centroid bounds
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -104,7 +109,7 @@ struct Builder {
                 if (cost < best) { best = cost; best_k = k; }
             }
             const double leaf_cost = b.area() * (double)count;
-            if (count <= BVH_MAX_LEAF && !(best + 0.5 * b.area() < leaf_cost)) return leaf_word(first, count);
+            if (count <= max_leaf && !(best + traversal_cost * b.area() < leaf_cost)) return leaf_word(first, count);
             if (best_k < 0) {
                 use_median = true;
             } else {
@@ -208,6 +213,9 @@ SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
     }
     Builder b;
     b.out = &out;
+    if (const char* e = std::getenv("HRT_BVH_MAX_LEAF")) b.max_leaf = std::max(1, std::min(15, std::atoi(e)));
+    if (const char* e = std::getenv("HRT_BVH_LEAF_DEPTH")) b.leaf_depth = (uint32_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("HRT_BVH_TRAVERSAL_COST")) b.traversal_cost = std::atof(e);
     bool any = false;
     for (size_t i = 0; i < n; i++) {
         const float* s = &cr[4 * i];

@@ -20,7 +20,8 @@
 #include "rt_device.hpp"
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
-hipError_t hrt_launch_queue(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 
 namespace {
 
@@ -120,6 +121,8 @@ struct rt_renderer {
     rt_stats stats{};
     bool timing_pending = false;
     int last_variant = 0;
+    std::vector<hipEvent_t> ev_trace;  // start/stop pairs around each k_trace launch of the last draw
+    uint32_t trace_pairs = 0;
     uint32_t last_schedule = 0;
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
@@ -237,6 +240,16 @@ int upload_spheres(rt_renderer* r) {
 }
 
 // variant 0 = the fastest exact scan for the scene: the culling BVH from 32 slots up, else the deferred scan.
+// Event pairs for `pairs + 1` k_trace launches (created on demand, kept for the renderer's life).
+int trace_events(rt_renderer* r, uint32_t pair) {
+    while (r->ev_trace.size() < 2u * (pair + 1u)) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        r->ev_trace.push_back(e);
+    }
+    return RT_OK;
+}
+
 // schedule 0 = the sample queue (load-balanced at sample granularity).
 uint32_t resolve_schedule(const rt_renderer* r) {
     return r->params.schedule ? r->params.schedule : RT_SCHEDULE_QUEUE;
@@ -353,9 +366,15 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
             P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * ((P.nframes + P.job_frames - 1u) / P.job_frames);
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
-            HIP_TRY(hrt_launch_queue(r->mode, variant, P, r->stream));
+            rc = trace_events(r, launches / 2u);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(r->ev_trace[launches], r->stream));
+            HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
+            HIP_TRY(hipEventRecord(r->ev_trace[launches + 1], r->stream));
+            HIP_TRY(hrt_launch_accumulate(P, r->stream));
             launches += 2;
         }
+        r->trace_pairs = launches / 2u;
     } else {
         const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
@@ -366,6 +385,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             HIP_TRY(hrt_launch_render(r->mode, variant, P, r->stream));
             launches++;
         }
+        r->trace_pairs = 0;  // k_render is the whole draw: trace time = kernel time
     }
     HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
     r->frame_count += count;  // end_frame, renderer.rs:409
@@ -385,6 +405,18 @@ int finish_stats(rt_renderer* r) {
     unsigned long long* q = r->raw_counters;
     HIP_TRY(hipMemcpy(q, r->counter.ptr, RT_RAW_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     r->stats.kernel_ms = ms;
+    r->stats.trace_ms = ms;
+    r->stats.trace_launches = r->stats.launches;
+    if (r->trace_pairs) {
+        double tms = 0.0;
+        for (uint32_t k = 0; k < r->trace_pairs; k++) {
+            float e = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&e, r->ev_trace[2 * k], r->ev_trace[2 * k + 1]));
+            tms += e;
+        }
+        r->stats.trace_ms = tms;
+        r->stats.trace_launches = r->trace_pairs;
+    }
     r->stats.queries = q[0];
     r->stats.box_tests = q[1];
     r->stats.sphere_tests = q[2];
@@ -431,7 +463,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
     r->params.queue_budget_mb = 4096;
-    r->params.job_frames = 4;
+    r->params.job_frames = 8;
     if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
         rt_destroy(r);
@@ -457,6 +489,7 @@ int rt_destroy(rt_renderer* r) {
     r->tris.release();
     r->mats.release();
     r->counter.release();
+    for (hipEvent_t e : r->ev_trace) (void)hipEventDestroy(e);
     if (r->ev_start) (void)hipEventDestroy(r->ev_start);
     if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
     if (r->stream) (void)hipStreamDestroy(r->stream);

@@ -56,6 +56,9 @@ class RtStats(C.Structure):
         ("schedule", C.c_uint32),
         ("node_tests", C.c_uint64),
         ("tri_tests", C.c_uint64),
+        ("trace_ms", C.c_double),
+        ("trace_launches", C.c_uint32),
+        ("pad1", C.c_uint32),
     ]
 
 

@@ -71,7 +71,7 @@ typedef struct rt_params {
                                   (persistent grid pulling (pixel, frame) samples + in-order fold);
                                   bit-identical                               */
     uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
-    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 4        */
+    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 8        */
 } rt_params;
 
 #define RT_SCHEDULE_AUTO 0u
@@ -90,6 +90,9 @@ typedef struct rt_stats {
     uint32_t schedule;     /* schedule the last draw call ran (RT_SCHEDULE_TILES / _QUEUE)             */
     uint64_t node_tests;   /* triangle program: implicit-heap node (slab) tests                         */
     uint64_t tri_tests;    /* triangle program: Moller-Trumbore tests                                   */
+    double trace_ms;       /* HIP-event time of the ray-tracing kernels alone (k_render / k_trace)      */
+    uint32_t trace_launches; /* launches of those kernels (the dominant kernel's launch count)          */
+    uint32_t pad1;
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

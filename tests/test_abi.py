@@ -52,7 +52,7 @@ def test_struct_layouts_match_header():
         fields = _header_struct(name)
         assert [(f, ctypes_of[t]) for t, f in fields] == list(py._fields_), name
     assert C.sizeof(hrt.RtParams) == 10 * 4
-    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8
+    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
 
