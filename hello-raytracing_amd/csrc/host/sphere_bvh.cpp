@@ -140,61 +140,6 @@ struct Builder {
     }
 };
 
-// Collapse of the BVH2 into 4-wide nodes: a node's children start as the BVH2 node's two children;
-// while fewer than four, the internal child with the largest box surface is replaced by its own two
-// children. Every child box is a BVH2 box, so the kernel's per-box padding argument is unchanged.
-struct Collapser {
-    SphereBvh* out;
-    uint32_t max_depth = 0;
-
-    uint32_t collapse(uint32_t word, uint32_t depth) {
-        if (word & BVH_LEAF_BIT) return word;
-        max_depth = std::max(max_depth, depth);
-        struct Child {
-            Box box;
-            uint32_t word;
-        };
-        Child c[4];
-        int n = 0;
-        auto add_children = [&](uint32_t w, int at) {
-            const SphereBvhNode& b = out->nodes[w];
-            Child l, r;
-            for (int k = 0; k < 3; k++) {
-                l.box.lo[k] = b.lmin[k]; l.box.hi[k] = b.lmax[k];
-                r.box.lo[k] = b.rmin[k]; r.box.hi[k] = b.rmax[k];
-            }
-            l.word = b.left;
-            r.word = b.right;
-            c[at] = l;
-            c[n++] = r;
-        };
-        n = 1;
-        add_children(word, 0);
-        while (n < 4) {
-            int pick = -1;
-            double best = -1.0;
-            for (int j = 0; j < n; j++)
-                if (!(c[j].word & BVH_LEAF_BIT) && c[j].box.area() > best) { best = c[j].box.area(); pick = j; }
-            if (pick < 0) break;
-            add_children(c[pick].word, pick);
-        }
-        const uint32_t idx = (uint32_t)out->nodes4.size();
-        out->nodes4.push_back(SphereBvh4Node{});
-        uint32_t words[4];
-        for (int j = 0; j < 4; j++) words[j] = j < n ? collapse(c[j].word, depth + 1) : BVH4_EMPTY;
-        SphereBvh4Node& q = out->nodes4[idx];
-        for (int j = 0; j < 4; j++) {
-            const bool used = j < n;
-            q.minx[j] = used ? c[j].box.lo[0] : 0.0f; q.maxx[j] = used ? c[j].box.hi[0] : 0.0f;
-            q.miny[j] = used ? c[j].box.lo[1] : 0.0f; q.maxy[j] = used ? c[j].box.hi[1] : 0.0f;
-            q.minz[j] = used ? c[j].box.lo[2] : 0.0f; q.maxz[j] = used ? c[j].box.hi[2] : 0.0f;
-            q.child[j] = words[j];
-            q.pad[j] = 0;
-        }
-        return idx;
-    }
-};
-
 }  // namespace
 
 SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
@@ -240,9 +185,6 @@ SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
     Box root;
     out.root_word = b.build(0, b.prims.size(), 0, &root);
     out.depth = b.max_depth;
-    Collapser col{&out};
-    out.root4_word = col.collapse(out.root_word, 0);
-    out.depth4 = col.max_depth;
     // leaf sphere data in BVH order
     out.sph.resize(out.slot.size() * 4);
     for (size_t k = 0; k < out.slot.size(); k++) {

@@ -24,20 +24,9 @@ struct SphereBvhNode {     // 64 B, both children's boxes stored in the parent
 };
 static_assert(sizeof(SphereBvhNode) == 64, "SphereBvhNode");
 
-// 4-wide node of the collapsed tree (variants 9/10): the boxes of up to four children, SoA so one
-// load per coordinate serves all four slab tests, then the four child words. Unused slots hold
-// BVH4_EMPTY (an empty leaf, which the kernel masks out).
-struct SphereBvh4Node {    // 128 B = one cache line
-    float minx[4], maxx[4], miny[4], maxy[4], minz[4], maxz[4];
-    uint32_t child[4];
-    uint32_t pad[4];
-};
-static_assert(sizeof(SphereBvh4Node) == 128, "SphereBvh4Node");
-
 constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
-constexpr uint32_t BVH4_EMPTY = 0x80000000u;  // leaf word with zero spheres
 constexpr uint32_t BVH_MAX_LEAF = 4;
-constexpr uint32_t BVH_MAX_DEPTH = 30;  // the kernel's traversal stack holds 32 entries
+constexpr uint32_t BVH_MAX_DEPTH = 30;  // informational; the kernel falls back to the exact scan on stack overflow
 
 struct SphereBvh {
     std::vector<SphereBvhNode> nodes;  // nodes[0] = root (empty when the tree holds < 2 spheres)
@@ -49,10 +38,6 @@ struct SphereBvh {
     float root_radius = 0;             // >= half-diagonal of the root box (rounded up)
     float r_min = 0, r_max = 0;        // radius range of the BVH spheres
     uint32_t depth = 0;
-    // the same tree collapsed to 4-wide nodes (leaves and boxes unchanged, only regrouped)
-    std::vector<SphereBvh4Node> nodes4;
-    uint32_t root4_word = 0x80000000u;
-    uint32_t depth4 = 0;
 };
 
 // centers_radii: 4 floats per slot (cx, cy, cz, radius). Slots with non-finite data go to `large`.

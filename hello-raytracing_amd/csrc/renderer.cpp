@@ -103,7 +103,7 @@ struct rt_renderer {
     DevBuf<hrt_dev::SpherePair> sph_pairs;
     uint32_t n_spheres = 0;
     // culling BVH over the sphere slots (SCAN_BVH)
-    DevBuf<float4> bvh_nodes, bvh4_nodes, bvh_sph;
+    DevBuf<float4> bvh_nodes, bvh_sph;
     DevBuf<int> bvh_slot, bvh_large;
     hrt::SphereBvh bvh_host;
     DevBuf<float4> nodes;
@@ -188,29 +188,11 @@ int upload_spheres(rt_renderer* r) {
         o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
         o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
     }
-    // 4-wide nodes: 8 float4 each (minx, maxx, miny, maxy, minz, maxz, child words, unused)
-    std::vector<float4> bnodes4(8 * std::max<size_t>(B.nodes4.size(), 1));
-    for (size_t j = 0; j < B.nodes4.size(); j++) {
-        const hrt::SphereBvh4Node& n = B.nodes4[j];
-        float* o = &bnodes4[8 * j].x;
-        for (int c = 0; c < 4; c++) {
-            const bool used = n.child[c] != hrt::BVH4_EMPTY;
-            o[0 + c] = used ? rel_lo(n.minx[c], 0) : 0.0f;
-            o[4 + c] = used ? rel_hi(n.maxx[c], 0) : 0.0f;
-            o[8 + c] = used ? rel_lo(n.miny[c], 1) : 0.0f;
-            o[12 + c] = used ? rel_hi(n.maxy[c], 1) : 0.0f;
-            o[16 + c] = used ? rel_lo(n.minz[c], 2) : 0.0f;
-            o[20 + c] = used ? rel_hi(n.maxz[c], 2) : 0.0f;
-            o[24 + c] = __builtin_bit_cast(float, n.child[c]);
-            o[28 + c] = 0.0f;
-        }
-    }
     const size_t nleaf = B.slot.size();
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
     if (!rc) rc = ensure(r->sph_pairs, npairs);
     if (!rc) rc = ensure(r->bvh_nodes, bnodes.size());
-    if (!rc) rc = ensure(r->bvh4_nodes, bnodes4.size());
     if (!rc) rc = ensure(r->bvh_sph, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_slot, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_large, std::max<size_t>(B.large.size(), 1));
@@ -221,8 +203,6 @@ int upload_spheres(rt_renderer* r) {
         HIP_TRY(hipMemcpyAsync(r->sph_pairs.ptr, pairs.data(), npairs * sizeof(pairs[0]), hipMemcpyHostToDevice,
                                r->stream));
         HIP_TRY(hipMemcpyAsync(r->bvh_nodes.ptr, bnodes.data(), bnodes.size() * sizeof(float4),
-                               hipMemcpyHostToDevice, r->stream));
-        HIP_TRY(hipMemcpyAsync(r->bvh4_nodes.ptr, bnodes4.data(), bnodes4.size() * sizeof(float4),
                                hipMemcpyHostToDevice, r->stream));
         if (nleaf) {
             HIP_TRY(hipMemcpyAsync(r->bvh_sph.ptr, B.sph.data(), nleaf * sizeof(float4), hipMemcpyHostToDevice,
@@ -322,8 +302,6 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.large_slots = r->bvh_large.ptr;
     P.nlarge = (uint32_t)B.large.size();
     P.bvh_root = B.root_word;
-    P.bvh4_nodes = r->bvh4_nodes.ptr;
-    P.bvh4_root = B.root4_word;
     for (int k = 0; k < 3; k++) P.bvh_rc[k] = B.root_center[k];
     P.bvh_rr = B.root_radius;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
@@ -332,15 +310,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.pad_k2 = B.r_min > 0.0f ? 16.0f * u / B.r_min : INFINITY;
     P.pad_k3 = 2e-3f;
     P.pad_k4 = 4.0f * u;
-    int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
-    // the lane state machine is sphere-program only and needs at least one bounce
-    if (variant == hrt_dev::SCAN_LANES && (r->mode != RT_MODE_SPHERE || P.bounces == 0)) variant = hrt_dev::SCAN_BVH;
-    // the LDS copy of the BVH holds at most BVH_LDS_NODES nodes
-    P.bvh_nnodes = (uint32_t)B.nodes.size();
-    if (variant == hrt_dev::SCAN_BVH_LDS && P.bvh_nnodes > (uint32_t)hrt_dev::BVH_LDS_NODES) variant = hrt_dev::SCAN_BVH;
+    const int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
     const uint32_t schedule = resolve_schedule(r);
-    if (schedule == RT_SCHEDULE_QUEUE && variant != hrt_dev::SCAN_SIMPLE && variant != hrt_dev::SCAN_DEFER)
-        variant = hrt_dev::SCAN_BVH;  // the queue kernels carry the simple, deferred and BVH scans
     r->last_variant = variant;
     r->last_schedule = schedule;
 
@@ -364,7 +335,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
             P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
-            P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * ((P.nframes + P.job_frames - 1u) / P.job_frames);
+            P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
+            P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
             rc = trace_events(r, launches / 2u);
             if (rc) return rc;
@@ -506,7 +478,8 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
-    if (p->variant > 10) return fail(RT_ERR_ARG, "rt_set_params: unknown variant");
+    if (p->variant != 0 && p->variant != 1 && p->variant != 3 && p->variant != 4)
+        return fail(RT_ERR_ARG, "rt_set_params: unknown variant (0 auto, 1 simple, 3 deferred, 4 culling BVH)");
     if (p->schedule > RT_SCHEDULE_QUEUE) return fail(RT_ERR_ARG, "rt_set_params: unknown schedule");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

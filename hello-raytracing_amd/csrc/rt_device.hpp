@@ -52,22 +52,13 @@ struct SpherePair {
 };
 static_assert(sizeof(SpherePair) == 32, "SpherePair");
 
-// Closest-sphere scan implementations (rt_params.variant).
+// Closest-sphere scan implementations (rt_params.variant). Variants 2 and 5-10 of earlier builds (packed
+// interval scan, while-while, lane state machine, LDS nodes, pop re-culling, 4-wide tree) were measured
+// slower than 4 and removed (history).
 constexpr int SCAN_SIMPLE = 1;  // one slot per iteration, exact sqrt/div whenever disc >= 0 && b < 0
-constexpr int SCAN_PACKED = 2;  // slot pairs, packed math, interval filter, exact sqrt/div only on ambiguity
 constexpr int SCAN_DEFER = 3;   // slot pairs, packed math, candidate list in LDS, exact resolution after
 constexpr int SCAN_BVH = 4;     // conservative BVH culling + exact tests, (t, slot) lexicographic min
-constexpr int SCAN_BVH_WW = 5;  // the same BVH, while-while traversal (leaves postponed wave-wide)
-constexpr int SCAN_LANES = 6;   // the same BVH, per-lane state machine with batched shading (sphere mode)
-constexpr int SCAN_BVH_LDS = 7; // variant 4 with the BVH nodes staged in LDS per workgroup
-constexpr int BVH_LDS_NODES = 320;  // node capacity of the LDS copy (20 KB)
-constexpr int BVH_STACK_LDS = 12;   // stack entries per lane for variant 7 (overflow -> exact full scan)
-constexpr int SCAN_BVH_CULL = 8;    // variant 4 + popped subtrees re-culled against the current best t
-constexpr int BVH_STACK_CULL = 12;  // (node word, entry distance) pairs per lane for variant 8
-constexpr int SCAN_BVH4 = 9;         // the culling tree collapsed to 4-wide nodes, sorted child order
-constexpr int SCAN_BVH4_CULL = 10;   // variant 9 + popped subtrees re-culled against the current best t
 constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
-constexpr uint32_t BVH4_EMPTY = 0x80000000u;  // unused child slot (empty leaf)
 #ifndef HRT_BVH_STACK
 #define HRT_BVH_STACK 24
 #endif
@@ -96,9 +87,6 @@ struct KParams {
     const int* bvh_slot;          // original slot of each leaf sphere
     const int* large_slots;       // slots scanned linearly for every ray
     uint32_t nlarge, bvh_root;    // large-list length, root child word
-    uint32_t bvh_nnodes;          // internal nodes (4 float4 each)
-    const float4* bvh4_nodes;     // the same tree collapsed 4-wide: 8 float4 per node (SphereBvh4Node)
-    uint32_t bvh4_root, pad_w;    // root child word of the 4-wide tree
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     const float4* nodes;          // 2 float4 per node: min, max
@@ -111,7 +99,7 @@ struct KParams {
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
-    uint32_t job_frames, pad_j;   // frames per job (a job = one tile x job_frames frames)
+    uint32_t job_frames, nchunks; // frames per job (a job = one tile x job_frames frames), chunks per tile
 };
 
 struct f3 {

@@ -95,79 +95,6 @@ __device__ __forceinline__ float exact_sphere_t(const KParams& P, const Ray& r, 
     return (-b - __builtin_sqrtf(disc)) / a2;
 }
 
-// Packed scan, bit-identical to scan_spheres. Two slots per iteration with v_pk_* math. A candidate
-// (disc >= 0, b <= 0) first gets an interval [ta - m, ta + m] from the hardware approximate sqrt and
-// reciprocal that provably contains the reference's correctly rounded t (error <= ~2^-19 (|b|+s)/(2a),
-// m = 2^-16 (|b|+s)/(2a) + 2^-60/(2a)); the correctly rounded sqrt/div run only when the interval cannot
-// decide the reference comparison (t > 0 && t < best, first slot wins ties). NaN/inf in the
-// approximation always falls through to the exact path.
-__device__ __forceinline__ int scan_spheres_packed(const KParams& P, const Ray& r, float& best) {
-    const float a = dot(r.d, r.d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
-    // The interval bound assumes a normal, non-huge 2a (v_rcp_f32 flushes outside that range).
-    if (!(a2 > 0x1p-100f && a2 < 0x1p100f)) return scan_spheres(P, r, best);
-    const float ra2 = __builtin_amdgcn_rcpf(a2);
-    const float mr = ra2 * 0x1p-16f, mc = ra2 * 0x1p-60f;
-    const v2f ox = {r.o.x, r.o.x}, oy = {r.o.y, r.o.y}, oz = {r.o.z, r.o.z};
-    const v2f dx = {r.d.x, r.d.x}, dy = {r.d.y, r.d.y}, dz = {r.d.z, r.d.z};
-    const v2f na4 = {-a4, -a4};
-    float lo_best = best, hi_best = best;  // bounds on the exact t of the current winner
-    bool exact_best = true;
-    int bi = -1;
-
-    auto candidate = [&](int i, float disc, float b) {
-        const float nb = -b;
-        const float s1 = __builtin_amdgcn_sqrtf(disc);
-        const float ta = (nb - s1) * ra2;
-        const float m = __builtin_fmaf(nb + s1, mr, mc);
-        const float lo = ta - m, hi = ta + m;
-        if (hi <= 0.0f) return;                      // t <= 0: rejected
-        if (lo > 0.0f && hi < lo_best) {             // certainly 0 < t < best
-            lo_best = lo; hi_best = hi; bi = i; exact_best = false;
-            return;
-        }
-        if (lo > 0.0f && lo >= hi_best) return;      // certainly t >= best (ties keep the earlier slot)
-        // ambiguous: decide with the reference's exact arithmetic
-        if (!exact_best) {
-            const float tb = exact_sphere_t(P, r, bi, a4, a2);
-            lo_best = hi_best = tb;
-            exact_best = true;
-        }
-        const float t = (nb - __builtin_sqrtf(disc)) / a2;
-        if (t > 0.0f && t < lo_best) {
-            lo_best = hi_best = t;
-            bi = i;
-        }
-    };
-
-    const SpherePair* __restrict__ pairs = P.sph_pairs;
-    const uint32_t np = P.npairs;
-#pragma unroll 2
-    for (uint32_t p = 0; p < np; p++) {
-        const SpherePair q = pairs[p];  // wave-uniform: scalar loads
-        const v2f ocx = ox - q.cx, ocy = oy - q.cy, ocz = oz - q.cz;
-        v2f bd = ocx * dx;
-        bd = __builtin_elementwise_fma(ocy, dy, bd);
-        bd = __builtin_elementwise_fma(ocz, dz, bd);
-        const v2f b = bd + bd;
-        v2f cd = ocx * ocx;
-        cd = __builtin_elementwise_fma(ocy, ocy, cd);
-        cd = __builtin_elementwise_fma(ocz, ocz, cd);
-        const v2f c = cd - q.rr;
-        const v2f disc = __builtin_elementwise_fma(b, b, na4 * c);
-        const float x0 = __builtin_fminf(disc.x, -b.x);
-        const float x1 = __builtin_fminf(disc.y, -b.y);
-        if (__builtin_fmaxf(x0, x1) >= 0.0f) {
-            if (x0 >= 0.0f) candidate((int)(2 * p), disc.x, b.x);
-            if (x1 >= 0.0f) candidate((int)(2 * p + 1), disc.y, b.y);
-        }
-    }
-    if (bi >= 0 && !exact_best) lo_best = exact_sphere_t(P, r, bi, a4, a2);
-    best = lo_best;
-    return bi;
-}
-
 // Deferred scan, bit-identical to scan_spheres. Pass 1 (uniform over all slot pairs, packed math)
 // only decides which pairs hold a candidate (disc >= 0 && b <= 0, or NaN: conservative) and appends
 // the pair index to this lane's list in LDS (ascending). Pass 2 resolves the few candidates with the
@@ -272,15 +199,9 @@ __device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx,
 // padded slab test visits (float-error bound on the discriminant, DESIGN.md §Sphere BVH exactness), every
 // visited sphere is tested with the reference arithmetic, and the winner is the (t, slot) minimum.
 // Rays the bound does not cover (non-finite origin, 2a outside [2^-100, 2^100]) or a stack overflow fall
-// back to the full exact scan.
-// `nodes` is P.bvh_nodes (global) or the workgroup's LDS copy of it (variant 7); `stack_cap` the per-lane
-// LDS stack depth.
-// CULL_POP: every stack entry also keeps the padded-box entry distance of its subtree (second half of the
-// stack area), and a popped subtree whose entry already exceeds the current best t is skipped without
-// loading it — the same strict `entry > best` criterion the visit test applies, so still exact.
-template <int STACK_CAP = BVH_STACK, bool CULL_POP = false>
+// back to the full exact scan. `stack` is this lane's slot of the workgroup's LDS stack (stride 256).
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
-                                                Tally& tally, const float4* __restrict__ nodes) {
+                                                Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a;
     const float a2 = 2.0f * a;
@@ -309,6 +230,7 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
     const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
 
+    const float4* __restrict__ nodes = P.bvh_nodes;
     uint32_t node = P.bvh_root;
     int sp = 0;
     bool overflow = false;
@@ -325,9 +247,8 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
-                if (sp < STACK_CAP) {
+                if (sp < BVH_STACK) {
                     stack[sp * 256] = lfirst ? right : left;
-                    if constexpr (CULL_POP) stack[(STACK_CAP + sp) * 256] = __float_as_uint(lfirst ? tr : tl);
                     sp++;
                 } else {
                     overflow = true;
@@ -346,235 +267,8 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             }
             tally.spheres += cnt;
         }
-        if constexpr (CULL_POP) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                if (__uint_as_float(stack[(STACK_CAP + sp) * 256]) <= bt) {
-                    node = stack[sp * 256];
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-        } else {
-            if (sp == 0) break;
-            node = stack[(--sp) * 256];
-        }
-    }
-    if (overflow) {
-        tally.spheres += P.nslots;
-        return scan_spheres(P, r, best);
-    }
-    best = bt;
-    return bi;
-}
-
-// Compare-exchange of (entry distance, child word) pairs into ascending distance.
-__device__ __forceinline__ void cx_pair(float& ta, uint32_t& wa, float& tb, uint32_t& wb) {
-    const bool sw = tb < ta;
-    const float t0 = sw ? tb : ta, t1 = sw ? ta : tb;
-    const uint32_t w0 = sw ? wb : wa, w1 = sw ? wa : wb;
-    ta = t0; tb = t1; wa = w0; wb = w1;
-}
-
-// Variants 9/10: the culling tree collapsed to 4-wide nodes (host/sphere_bvh.cpp Collapser). One
-// iteration tests the four child boxes of a node (SoA loads, the same padded slab test and boxes as
-// variant 4), sorts the hit children by entry distance, continues into the nearest and pushes the rest
-// farthest-first. Same exactness argument as scan_spheres_bvh; only the visiting order differs, and the
-// (t, slot) lexicographic minimum is order-independent.
-template <int STACK_CAP, bool CULL_POP>
-__device__ __forceinline__ int scan_spheres_bvh4(const KParams& P, const Ray& r, float& best, uint32_t* stack,
-                                                 Tally& tally) {
-    const float a = dot(r.d, r.d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
-    const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
-    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
-        tally.spheres += P.nslots;
-        return scan_spheres(P, r, best);
-    }
-    float bt = best;
-    int bi = -1;
-    for (uint32_t k = 0; k < P.nlarge; k++) {
-        const int i = P.large_slots[k];
-        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
-        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-    }
-    tally.spheres += P.nlarge;
-
-    const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
-    const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
-    const float D = dl * 1.001f + P.bvh_rr;
-    const float dn = __builtin_amdgcn_sqrtf(a);
-    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
-    const float pad = 2.02f * delta;
-    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
-    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
-    const float4* __restrict__ nodes = P.bvh4_nodes;
-
-    uint32_t node = P.bvh4_root;
-    int sp = 0;
-    bool overflow = false;
-    while (true) {
-        if (!(node & BVH_LEAF_BIT)) {
-            const float4* nd = nodes + 8u * node;
-            const float4 mnx = nd[0], mxx = nd[1], mny = nd[2], mxy = nd[3], mnz = nd[4], mxz = nd[5];
-            const float4 cw = nd[6];
-            float t[4];
-            uint32_t w[4];
-            const float mnxa[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, mxxa[4] = {mxx.x, mxx.y, mxx.z, mxx.w};
-            const float mnya[4] = {mny.x, mny.y, mny.z, mny.w}, mxya[4] = {mxy.x, mxy.y, mxy.z, mxy.w};
-            const float mnza[4] = {mnz.x, mnz.y, mnz.z, mnz.w}, mxza[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
-            const float cwa[4] = {cw.x, cw.y, cw.z, cw.w};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                float te;
-                const bool h = padded_box_hit(make_float4(mnxa[c], mnya[c], mnza[c], 0.0f),
-                                              make_float4(mxxa[c], mxya[c], mxza[c], 0.0f), lo, hi, inv, bt, te);
-                w[c] = __float_as_uint(cwa[c]);
-                t[c] = (h && w[c] != BVH4_EMPTY) ? te : __builtin_inff();
-                tally.boxes += w[c] != BVH4_EMPTY;
-            }
-            cx_pair(t[0], w[0], t[1], w[1]);
-            cx_pair(t[2], w[2], t[3], w[3]);
-            cx_pair(t[0], w[0], t[2], w[2]);
-            cx_pair(t[1], w[1], t[3], w[3]);
-            cx_pair(t[1], w[1], t[2], w[2]);
-            if (t[0] != __builtin_inff()) {
-#pragma unroll
-                for (int c = 3; c >= 1; c--) {
-                    if (t[c] != __builtin_inff()) {
-                        if (sp < STACK_CAP) {
-                            stack[sp * 256] = w[c];
-                            if constexpr (CULL_POP) stack[(STACK_CAP + sp) * 256] = __float_as_uint(t[c]);
-                            sp++;
-                        } else {
-                            overflow = true;
-                        }
-                    }
-                }
-                node = w[0];
-                continue;
-            }
-        } else {
-            const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
-            for (uint32_t j = 0; j < cnt; j++) {
-                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
-                const int i = P.bvh_slot[first + j];
-                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-            }
-            tally.spheres += cnt;
-        }
-        if constexpr (CULL_POP) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                if (__uint_as_float(stack[(STACK_CAP + sp) * 256]) <= bt) {
-                    node = stack[sp * 256];
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-        } else {
-            if (sp == 0) break;
-            node = stack[(--sp) * 256];
-        }
-    }
-    if (overflow) {
-        tally.spheres += P.nslots;
-        return scan_spheres(P, r, best);
-    }
-    best = bt;
-    return bi;
-}
-
-// Variant 5: the same culling BVH and exactness argument as scan_spheres_bvh, traversed "while-while"
-// (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps walking internal nodes until every
-// lane of the wave holds a leaf (or has nothing left), then the wave tests leaves together. This keeps the
-// internal-node and leaf code paths from both running in nearly every iteration.
-constexpr uint32_t BVH_DONE = 0xFFFFFFFFu;
-
-__device__ __forceinline__ int scan_spheres_bvh_ww(const KParams& P, const Ray& r, float& best, uint32_t* stack,
-                                                   Tally& tally) {
-    const float a = dot(r.d, r.d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
-    const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
-    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
-        tally.spheres += P.nslots;
-        return scan_spheres(P, r, best);
-    }
-    float bt = best;
-    int bi = -1;
-    for (uint32_t k = 0; k < P.nlarge; k++) {
-        const int i = P.large_slots[k];
-        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
-        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-    }
-    tally.spheres += P.nlarge;
-
-    const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
-    const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
-    const float D = dl * 1.001f + P.bvh_rr;
-    const float dn = __builtin_amdgcn_sqrtf(a);
-    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
-    const float pad = 2.02f * delta;
-    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
-    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
-
-    uint32_t node = P.bvh_root, leaf = 0;
-    int sp = 0;
-    bool overflow = false;
-    auto pop = [&]() -> uint32_t { return sp > 0 ? stack[(--sp) * 256] : BVH_DONE; };
-    while (true) {
-        // internal-node phase
-        while (true) {
-            while (node != BVH_DONE && (node & BVH_LEAF_BIT) && leaf == 0) {  // postpone a leaf
-                leaf = node;
-                node = pop();
-            }
-            const bool internal = node != BVH_DONE && !(node & BVH_LEAF_BIT);
-            if (__all(!internal || leaf != 0)) break;  // every lane holds a leaf or cannot descend
-            if (internal) {
-                const float4 n0 = P.bvh_nodes[4 * node + 0];
-                const float4 n1 = P.bvh_nodes[4 * node + 1];
-                const float4 n2 = P.bvh_nodes[4 * node + 2];
-                const float4 n3 = P.bvh_nodes[4 * node + 3];
-                float tl, tr;
-                const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
-                const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
-                tally.boxes += 2;
-                const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
-                if (hl && hr) {
-                    const bool lfirst = tl <= tr;
-                    if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
-                    else overflow = true;
-                    node = lfirst ? left : right;
-                } else if (hl) {
-                    node = left;
-                } else if (hr) {
-                    node = right;
-                } else {
-                    node = pop();
-                }
-            }
-        }
-        // leaf phase
-        if (leaf != 0) {
-            const uint32_t first = (leaf >> 4) & 0x07FFFFFFu, cnt = leaf & 15u;
-            for (uint32_t j = 0; j < cnt; j++) {
-                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
-                const int i = P.bvh_slot[first + j];
-                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-            }
-            tally.spheres += cnt;
-            leaf = 0;
-        }
-        if (__all(node == BVH_DONE)) break;
+        if (sp == 0) break;
+        node = stack[(--sp) * 256];
     }
     if (overflow) {
         tally.spheres += P.nslots;
@@ -662,29 +356,15 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h,
 }
 
 template <int MODE, int SCAN>
-__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally,
-                                            const float4* lds_nodes) {
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally) {
     h.t = FLT_MAX_REF;
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
         int bi;
-        if constexpr (SCAN == SCAN_BVH_WW) {
-            bi = scan_spheres_bvh_ww(P, r, best, (uint32_t*)lds, tally);
-        } else if constexpr (SCAN == SCAN_BVH) {
-            bi = scan_spheres_bvh<BVH_STACK>(P, r, best, (uint32_t*)lds, tally, P.bvh_nodes);
-        } else if constexpr (SCAN == SCAN_BVH_LDS) {
-            bi = scan_spheres_bvh<BVH_STACK_LDS>(P, r, best, (uint32_t*)lds, tally, lds_nodes);
-        } else if constexpr (SCAN == SCAN_BVH_CULL) {
-            bi = scan_spheres_bvh<BVH_STACK_CULL, true>(P, r, best, (uint32_t*)lds, tally, P.bvh_nodes);
-        } else if constexpr (SCAN == SCAN_BVH4) {
-            bi = scan_spheres_bvh4<BVH_STACK, false>(P, r, best, (uint32_t*)lds, tally);
-        } else if constexpr (SCAN == SCAN_BVH4_CULL) {
-            bi = scan_spheres_bvh4<BVH_STACK_CULL, true>(P, r, best, (uint32_t*)lds, tally);
+        if constexpr (SCAN == SCAN_BVH) {
+            bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_DEFER) {
             bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
-            tally.spheres += P.nslots;
-        } else if constexpr (SCAN == SCAN_PACKED) {
-            bi = scan_spheres_packed(P, r, best);
             tally.spheres += P.nslots;
         } else {
             bi = scan_spheres(P, r, best);
@@ -783,36 +463,19 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 
 }  // namespace
 
-// One launch = P.nframes frames over this renderer's rows. Grid: (ceil(W/16), ceil(nrows/16)).
-#ifdef HRT_WAVES_PER_EU
-#define HRT_OCC __attribute__((amdgpu_waves_per_eu(HRT_WAVES_PER_EU)))
-#else
-#define HRT_OCC
-#endif
+// Tiles schedule (rt_params.schedule = RT_SCHEDULE_TILES): one launch = P.nframes frames over this
+// renderer's rows; a lane owns one pixel for all of them and accumulates in registers.
+// Grid: (ceil(W/16), ceil(nrows/16)).
 template <int MODE, int SCAN>
-__global__ __launch_bounds__(256) HRT_OCC void k_render(const KParams P) {
+__global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* lds_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
-    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVH_WW || SCAN == SCAN_BVH4) {
+    } else if constexpr (SCAN == SCAN_BVH) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
         lds_list = bvh_stack + threadIdx.x;
-    }
-    if constexpr (SCAN == SCAN_BVH_CULL || SCAN == SCAN_BVH4_CULL) {
-        __shared__ uint32_t bvh_stack_c[2 * BVH_STACK_CULL * 256];
-        lds_list = bvh_stack_c + threadIdx.x;
-    }
-    const float4* lds_nodes = nullptr;
-    if constexpr (SCAN == SCAN_BVH_LDS) {
-        // the culling BVH (<= BVH_LDS_NODES nodes, checked by the host) staged once per workgroup
-        __shared__ uint32_t bvh_stack_s[BVH_STACK_LDS * 256];
-        __shared__ float4 nodes_s[4 * BVH_LDS_NODES];
-        lds_list = bvh_stack_s + threadIdx.x;
-        for (uint32_t i = threadIdx.x; i < 4u * P.bvh_nnodes; i += 256u) nodes_s[i] = P.bvh_nodes[i];
-        __syncthreads();
-        lds_nodes = nodes_s;
     }
     Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
@@ -852,7 +515,7 @@ __global__ __launch_bounds__(256) HRT_OCC void k_render(const KParams P) {
 #endif
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, lds_nodes);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
             queries++;
 #ifdef HRT_STAMPS
             st_tb = hrt_stamp();
@@ -948,191 +611,6 @@ __global__ __launch_bounds__(256) HRT_OCC void k_render(const KParams P) {
     }
 }
 
-// Variant 6 — sphere program with the culling BVH of variant 4, scheduled as a per-lane state machine.
-// Every iteration of the outer loop advances each traversing lane by ONE traversal step (an internal node
-// or a leaf); lanes whose traversal has finished wait, and the wave shades them in a batch (hit record,
-// scatter, accumulation, next sample's primary ray, start of the next query) once at least
-// LANES_SHADE_BATCH lanes wait or nobody is traversing. A lane therefore never idles behind the wave's
-// longest traversal, and the shading code runs for many lanes at once. Per lane the sequence of
-// operations is exactly variant 4's, so the results are bit-identical.
-constexpr int LANES_SHADE_BATCH = 24;
-
-__global__ __launch_bounds__(256) void k_render_lanes(const KParams P) {
-    constexpr int MODE = MODE_SPHERE;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-    uint32_t* stack = bvh_stack + threadIdx.x;
-    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
-    const bool valid = x < P.W && kr < P.nrows;
-    const uint32_t y = P.row0 + kr * P.row_step;
-    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
-    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
-    if (valid) {
-        acc0 = px[0];
-        acc1 = px[1];
-        acc2 = px[2];
-    }
-    Tally tally;
-    uint32_t queries = 0;
-    uint32_t f = 0;
-
-    // path state
-    Ray ray;
-    f3 att = mk(1.0f, 1.0f, 1.0f);
-    float sky_t = 0.0f;
-    uint32_t s = 0, bounce = 0;
-    // query / traversal state
-    float a4 = 0.0f, a2 = 0.0f, bt = FLT_MAX_REF;
-    int bi = -1;
-    f3 inv = mk(0, 0, 0), lo = mk(0, 0, 0), hi = mk(0, 0, 0);
-    uint32_t node = BVH_DONE;
-    int sp = 0;
-    bool overflow = false;
-    int state = 2;  // 0 traversing, 1 waiting for shading, 2 finished
-
-    auto begin_query = [&]() {
-        queries++;
-        const float a = dot(ray.d, ray.d);
-        a4 = 4.0f * a;
-        a2 = 2.0f * a;
-        bt = FLT_MAX_REF;
-        bi = -1;
-        const bool finite_o =
-            __builtin_isfinite(ray.o.x) && __builtin_isfinite(ray.o.y) && __builtin_isfinite(ray.o.z);
-        if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {  // outside the padding bound: exact scan
-            bi = scan_spheres(P, ray, bt);
-            tally.spheres += P.nslots;
-            state = 1;
-            return;
-        }
-        for (uint32_t k = 0; k < P.nlarge; k++) {
-            const int i = P.large_slots[k];
-            const float t = exact_t_geo(P.sph_geo[i], ray, a4, a2);
-            if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-        }
-        tally.spheres += P.nlarge;
-        const f3 op = mk(ray.o.x - P.bvh_rc[0], ray.o.y - P.bvh_rc[1], ray.o.z - P.bvh_rc[2]);
-        const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
-        const float D = dl * 1.001f + P.bvh_rr;
-        const float dn = __builtin_amdgcn_sqrtf(a);
-        const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
-        const float pad = 2.02f * delta;
-        inv = mk(robust_inv(ray.d.x), robust_inv(ray.d.y), robust_inv(ray.d.z));
-        lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-        hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
-        node = P.bvh_root;
-        sp = 0;
-        overflow = false;
-        state = 0;
-    };
-    auto start_sample = [&]() {
-        ray = primary_ray<MODE>(P, x, y, P.time0 + f * P.dtime, s);
-        sky_t = ray.d.y * 0.5f + 0.5f;
-        att = mk(1.0f, 1.0f, 1.0f);
-        bounce = 0;
-    };
-
-    if (valid && P.nframes > 0) {  // the host routes bounces == 0 to another variant
-        start_sample();
-        begin_query();
-    }
-
-    while (true) {
-        if (state == 0) {  // one traversal step
-            bool finished = false;
-            if (!(node & BVH_LEAF_BIT)) {
-                const float4 n0 = P.bvh_nodes[4 * node + 0];
-                const float4 n1 = P.bvh_nodes[4 * node + 1];
-                const float4 n2 = P.bvh_nodes[4 * node + 2];
-                const float4 n3 = P.bvh_nodes[4 * node + 3];
-                float tl, tr;
-                const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
-                const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
-                tally.boxes += 2;
-                const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
-                if (hl && hr) {
-                    const bool lfirst = tl <= tr;
-                    if (sp < BVH_STACK) stack[(sp++) * 256] = lfirst ? right : left;
-                    else overflow = true;
-                    node = lfirst ? left : right;
-                } else if (hl) {
-                    node = left;
-                } else if (hr) {
-                    node = right;
-                } else {
-                    finished = sp == 0;
-                    if (!finished) node = stack[(--sp) * 256];
-                }
-            } else {
-                const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
-                for (uint32_t j = 0; j < cnt; j++) {
-                    const float t = exact_t_geo(P.bvh_sph[first + j], ray, a4, a2);
-                    const int i = P.bvh_slot[first + j];
-                    if (beats(t, i, bt, bi)) { bt = t; bi = i; }
-                }
-                tally.spheres += cnt;
-                finished = sp == 0;
-                if (!finished) node = stack[(--sp) * 256];
-            }
-            if (finished) {
-                if (overflow) {  // stack overflow: exact full scan decides
-                    bt = FLT_MAX_REF;
-                    bi = scan_spheres(P, ray, bt);
-                    tally.spheres += P.nslots;
-                }
-                state = 1;
-            }
-        }
-        const unsigned long long waiting = __ballot(state == 1), walking = __ballot(state == 0);
-        if (!waiting && !walking) break;
-        if (walking && __popcll(waiting) < LANES_SHADE_BATCH) continue;
-        if (state == 1) {  // shade: trace() loop body + fs_main accumulation, then the next query
-            bool done = true;
-            if (bi >= 0) {
-                Hit h;
-                sphere_record(P, ray, bi, bt, h);
-                scatter<MODE>(s, ray, h);
-                att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
-                bounce++;
-                done = bounce >= P.bounces;
-            }
-            if (done) {
-                const float u = 1.0f - sky_t;
-                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
-                const f3 c = att * sky;
-                const float fc = (float)(P.frame0 + f);
-                const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
-                const float omw = 1.0f - w;
-                acc0 = acc0 * omw + (0.0f + c.x) * w;
-                acc1 = acc1 * omw + (0.0f + c.y) * w;
-                acc2 = acc2 * omw + (0.0f + c.z) * w;
-                f++;
-                if (f < P.nframes) start_sample();
-            }
-            if (f < P.nframes) begin_query();
-            else state = 2;
-        }
-    }
-
-    if (valid) {
-        px[0] = acc0;
-        px[1] = acc1;
-        px[2] = acc2;
-    }
-    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
-#pragma unroll
-    for (int c = 0; c < 5; c++) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------
 // Sample-queue schedule (rt_params.schedule = RT_SCHEDULE_QUEUE). The tiles schedule (k_render) gives
 // every lane one pixel for all frames of a launch, so a pixel whose paths are long (glass, crevices:
@@ -1162,7 +640,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
     Tally tally;
     uint32_t queries = 0;
-    const uint32_t ntiles = P.tiles_w * P.tiles_h;
     const unsigned long long below = (1ull << lane) - 1ull;
 
     // wave-uniform job state
@@ -1174,7 +651,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     float sky_t = 0.0f;
     uint32_t s = 0, bounce = 0, x = 0, kr = 0, fl = 0;
     bool have = false;
+#ifdef HRT_STAMPS
+    unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb;
+    const unsigned long long st_start = hrt_stamp();
+    const unsigned long long rt_start = hrt_realtime();
+#endif
     while (true) {
+#ifdef HRT_STAMPS
+        st_ta = hrt_stamp();
+#endif
         // refill: free lanes take the next samples of the wave's job, fetching jobs as they run out
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
@@ -1187,8 +672,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                     drained = true;
                     break;
                 }
-                const uint32_t chunk = (uint32_t)(j / ntiles);
-                job_tile = (uint32_t)(j % ntiles);
+                // tile-major job order: one tile's frame chunks are handed out together and run on
+                // neighbouring waves at once, so an expensive tile finishes early instead of trailing
+                const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                job_tile = (uint32_t)(j / P.nchunks);
                 job_f0 = chunk * P.job_frames;
                 job_total = 64u * min(P.job_frames, P.nframes - job_f0);
                 job_next = 0;
@@ -1215,13 +702,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             job_next += took;
             m = __ballot(need);
         }
+#ifdef HRT_STAMPS
+        st_tb = hrt_stamp();
+        if (have) st_gen += st_tb - st_ta;
+#endif
         if (drained && __ballot(have) == 0ull) break;
         if (!have) continue;
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, nullptr);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
             queries++;
+#ifdef HRT_STAMPS
+            st_ta = hrt_stamp();
+            st_trav += st_ta - st_tb;
+            st_tb = st_ta;
+#endif
             if (hit) {
                 scatter<MODE>(s, ray, h);
                 att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
@@ -1240,7 +736,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             o[2] = c.z;
             have = false;
         }
+#ifdef HRT_STAMPS
+        st_shade += hrt_stamp() - st_tb;
+#endif
     }
+#ifdef HRT_STAMPS
+    {
+        // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
+        // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)
+        unsigned long long v[5] = {st_trav, st_shade, st_gen, hrt_stamp() - st_start, queries};
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
+        }
+        if (lane == 0) {
+            for (int c = 0; c < 4; c++) atomicAdd(P.counter + 8 + c, v[c]);
+            const unsigned long long t1 = hrt_stamp(), r1 = hrt_realtime();
+            atomicAdd(P.counter + 12, r1 - rt_start);
+            atomicAdd(P.counter + 13, 1ull);
+            atomicAdd(P.counter + 14, t1 - st_start);
+        }
+    }
+#endif
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
@@ -1325,36 +843,23 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Host-side launcher (called from renderer.cpp; no HIP types in the C-ABI). variant: SCAN_* (0 = default).
+// Host-side launcher of the tiles schedule (called from renderer.cpp; no HIP types in the C-ABI).
+// variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host).
 hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((P.W + 15u) / 16u, (P.nrows + 15u) / 16u);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    // variant 0 is resolved by the host (renderer.cpp) before the launch
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_SIMPLE>), grid, block, 0, stream, P);
-        else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_PACKED>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_WW>), grid, block, 0, stream, P);
-        else if (variant == SCAN_LANES) hipLaunchKernelGGL(k_render_lanes, grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_LDS>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH_CULL>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH4) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH4>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH4_CULL) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH4_CULL>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
+        else if (variant == SCAN_DEFER) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
         break;
     case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
     default:
         if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_SIMPLE>), grid, block, 0, stream, P);
-        else if (variant == SCAN_PACKED) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_PACKED>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_WW) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_WW>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_LDS) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_LDS>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH_CULL) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH_CULL>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH4) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH4>), grid, block, 0, stream, P);
-        else if (variant == SCAN_BVH4_CULL) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH4_CULL>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
+        else if (variant == SCAN_DEFER) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
         break;
     }
     return hipGetLastError();

@@ -61,11 +61,8 @@ typedef struct rt_params {
     uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
     uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots up, else 3), 1 simple,
-                                  2 packed + interval filter, 3 packed + deferred exact candidates,
-                                  4 conservative culling BVH, 5 BVH while-while, 6 BVH lane state
-                                  machine, 7 BVH nodes in LDS, 8 BVH + pop re-culling, 9 the BVH
-                                  collapsed 4-wide, 10 4-wide + pop re-culling; all bit-identical
-                                                                                   */
+                                  3 packed + deferred exact candidates, 4 conservative culling BVH;
+                                  all bit-identical. 2 and 5-10 were removed.    */
     uint32_t schedule;         /* work schedule of rt_draw_frames: 0 auto, 1 tiles (one lane per pixel
                                   for a launch's frames, in-register accumulation), 2 sample queue
                                   (persistent grid pulling (pixel, frame) samples + in-order fold);
@@ -86,7 +83,7 @@ typedef struct rt_stats {
     uint32_t local_rows;   /* rows owned by this renderer                                              */
     uint64_t box_tests;    /* padded-box tests of the sphere culling BVH (variant 4), last draw call    */
     uint64_t sphere_tests; /* ray-sphere tests (slots scanned, or BVH leaf + large-list tests)          */
-    uint32_t variant;      /* sphere-scan variant the last draw call ran (1..10)                        */
+    uint32_t variant;      /* sphere-scan variant the last draw call ran (1, 3, 4)                       */
     uint32_t schedule;     /* schedule the last draw call ran (RT_SCHEDULE_TILES / _QUEUE)             */
     uint64_t node_tests;   /* triangle program: implicit-heap node (slab) tests                         */
     uint64_t tri_tests;    /* triangle program: Moller-Trumbore tests                                   */

@@ -53,7 +53,8 @@ def main() -> None:
     ap.add_argument("--config", default="c3")
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--variants", type=int, nargs="+", default=[4])
-    ap.add_argument("--fpl", type=int, nargs="+", default=[32], help="frames per launch")
+    ap.add_argument("--fpl", type=int, nargs="+", default=[32], help="frames per launch (tiles schedule)")
+    ap.add_argument("--schedule", type=int, default=2, help="1 tiles (k_render), 2 sample queue (k_trace)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--trace", default=None, help="directory for per-wave records (.npy)")
     a = ap.parse_args()
@@ -64,7 +65,7 @@ def main() -> None:
     rows = []
     for v, fpl in [(v, f) for v in a.variants for f in a.fpl]:
         r = make_renderer(sd)
-        r.set_params(variant=v, frames_per_launch=fpl)
+        r.set_params(variant=v, frames_per_launch=fpl, schedule=a.schedule)
         r.draw_frames(2, 1000, 10)  # warm-up
         r.synchronize()
         r.draw_frames(a.frames, 1000, 10)
@@ -82,9 +83,9 @@ def main() -> None:
             # resident waves per SIMD over the draw (wave-lifetime sum / (draw time x 1024 SIMDs))
             "memtime_mhz": 100.0 * q[14] / max(1, q[12]),
             "waves": int(q[13]),
-            "resident_waves_per_simd": (q[12] / 1e8) / (st.kernel_ms / 1e3) / 1024.0,
+            "resident_waves_per_simd": (q[12] / 1e8) / (st.trace_ms / 1e3) / 1024.0,
         }
-        if a.trace:
+        if a.trace and a.schedule == 1:
             import numpy as np
             nw = 4 * ((sd.width + 15) // 16) * ((sd.height + 15) // 16) * 4
             buf = (hrt._lib.C.c_uint64 * nw)()

@@ -210,17 +210,19 @@ def test_rtiow_cover_scene_small():
     assert r.stats().queries == q
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
-def test_scan_variants_bit_identical(variant):
-    """Every sphere-scan kernel variant gives the same bits (and ray counts) as the oracle."""
+@pytest.mark.parametrize("schedule", [1, 2])
+@pytest.mark.parametrize("variant", [1, 3, 4])
+def test_scan_variants_bit_identical(variant, schedule):
+    """Every sphere-scan kernel variant, under both schedules, gives the oracle's bits and ray counts."""
     for sd in (scenes.config_c3(192, 108, 4), scenes.golden_scene("dielectric_materials", 128, 128),
                scenes.golden_scene("complex_scene", 128, 128)):
         sd.frames = 4
         r = scenes.make_renderer(sd)
-        r.set_params(variant=variant, schedule=1)
+        r.set_params(variant=variant, schedule=schedule)
         r.draw_frames(sd.frames, 1000, 10)
         ref, q = scenes.oracle_render(sd)
-        assert_parity(r.read_image(), ref, f"{sd.name} variant {variant}")
+        assert_parity(r.read_image(), ref, f"{sd.name} variant {variant} schedule {schedule}")
+        assert r.stats().variant == variant and r.stats().schedule == schedule
         assert r.stats().queries == q
 
 
@@ -228,7 +230,7 @@ def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
     imgs = []
-    for variant in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
+    for variant in (1, 3, 4):
         r = scenes.make_renderer(sd)
         r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
@@ -272,12 +274,12 @@ def _random_scene(kind: str, seed: int):
 def test_culling_bvh_exact_on_adversarial_scenes(kind):
     sd = _random_scene(kind, 7)
     out = []
-    for variant in (1, 4, 5, 6, 7, 8, 9, 10):
+    for variant in (1, 4):
         r = scenes.make_renderer(sd)
         r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
         out.append((r.read_image(), r.stats()))
-    for (img, st), v in zip(out[1:], (4, 5, 6, 7, 8, 9, 10)):
+    for (img, st), v in zip(out[1:], (4,)):
         np.testing.assert_array_equal(out[0][0].view(np.uint32), img.view(np.uint32))
         assert out[0][1].queries == st.queries
         assert st.variant == v and st.sphere_tests < out[0][1].sphere_tests
@@ -290,7 +292,7 @@ def test_culling_bvh_with_zero_radius_slots():
     sd = scenes.golden_scene("complex_scene", 96, 64)
     sd.frames = 6
     out = []
-    for variant in (1, 4, 5, 6, 7, 8, 9, 10):
+    for variant in (1, 4):
         r = scenes.make_renderer(sd)  # 25 spheres + 75 zero slots = 100 slots
         r.set_params(variant=variant, schedule=1)
         r.draw_frames(sd.frames, 1000, 10)
