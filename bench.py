@@ -213,14 +213,17 @@ def main() -> int:
                     / nl / (avg_launch_ms * 1e-3) / 1e12)
         px = local_rows * sd.width
         if schedule == 2:  # k_trace writes one 12 B colour per sample; the sphere arrays are read once
-            alg_bytes = 12.0 * px * sd.frames * args.steps / nl + 64.0 * nslots
+            alg_bytes = 12.0 * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
         else:  # k_render reads and writes the framebuffer once per launch
             alg_bytes = 24.0 * px + 64.0 * nslots
         traffic = None
         pmc = ROOT / "profiles" / "pmc_summary.json"
         if pmc.exists():
-            try:
-                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            try:  # the committed PMC pass (scripts/pmc.sh) of this same configuration and kernel
+                pm = json.loads(pmc.read_text())
+                kname = "k_trace" if schedule == 2 else "k_render"
+                if pm.get("_bench_config") == args.config and any(kname in k for k in pm.get("_kernels", [])):
+                    traffic = pm.get("hbm_bytes_per_launch")
             except Exception:  # noqa: BLE001
                 traffic = None
         out = {

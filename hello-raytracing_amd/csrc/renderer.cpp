@@ -111,7 +111,7 @@ struct rt_renderer {
     DevBuf<hrt_dev::MatDev> mats;
     uint32_t bvh_n = 0, bvh_m = 0;
     DevBuf<unsigned long long> counter;
-    DevBuf<float> samples;  // sample-queue colour buffer (frames x rows x W x 3)
+    DevBuf<float> samples;  // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
 
@@ -318,7 +318,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     uint32_t launches = 0;
     if (schedule == RT_SCHEDULE_QUEUE) {
         // frames per chunk: as many as the colour buffer budget holds
-        const size_t frame_floats = (size_t)P.nrows * r->width * 3u;
+        P.tiles_w = (r->width + 7u) / 8u;
+        P.tiles_h = (P.nrows + 7u) / 8u;
+        const size_t frame_floats = (size_t)P.tiles_w * P.tiles_h * 64u * 3u;  // tile-padded
         const size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
         const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
         if (count) {
@@ -327,8 +329,6 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         }
         P.samples = r->samples.ptr;
         P.queue = r->counter.ptr + 15;
-        P.tiles_w = (r->width + 7u) / 8u;
-        P.tiles_h = (P.nrows + 7u) / 8u;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
         for (uint32_t done = 0; done < count; done += chunk) {
             P.nframes = std::min(chunk, count - done);

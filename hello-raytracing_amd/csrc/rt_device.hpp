@@ -95,7 +95,7 @@ struct KParams {
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
     unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
     // sample-queue schedule (k_trace / k_accumulate)
-    float* samples;               // nframes x nrows x W x 3 sample colours, frame-major
+    float* samples;               // nframes x (tiles_w * tiles_h) x 64 px x 3 colours, frame- then tile-major
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows

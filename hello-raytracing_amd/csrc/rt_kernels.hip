@@ -623,7 +623,8 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // next job as soon as the current one has no samples left, while older samples are still in flight.
 // Lanes therefore never idle until the queue is empty, a wave's lanes stay inside one tile (ray
 // coherence: an incoherent sample queue measured 2.65x slower on C3), and one tile's frames are
-// spread over many waves. Each sample's colour goes to a frame-major buffer; k_accumulate then folds
+// spread over many waves. Each sample's colour goes to a frame-major, tile-major buffer (a tile's frame is
+// 768 contiguous bytes, so colour stores fill whole cache lines); k_accumulate then folds
 // the colours into the image in frame order per pixel with the reference's mix
 // (shader_sphere.wgsl:264-271), so the image is bit-identical to k_render's and to count x rt_draw.
 template <int MODE, int SCAN>
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     Ray ray;
     f3 att = mk(1.0f, 1.0f, 1.0f);
     float sky_t = 0.0f;
-    uint32_t s = 0, bounce = 0, x = 0, kr = 0, fl = 0;
+    uint32_t s = 0, bounce = 0, pix = 0, fl = 0;  // pix = tile * 64 + pixel-in-tile
     bool have = false;
 #ifdef HRT_STAMPS
     unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb;
@@ -686,8 +687,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 const uint32_t sid = job_next + rank;
                 const uint32_t l = sid & 63u;
                 fl = job_f0 + (sid >> 6);
-                x = (job_tile % P.tiles_w) * 8u + (l & 7u);
-                kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
+                pix = job_tile * 64u + l;
+                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
+                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
                 need = false;
                 if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
                     const uint32_t y = P.row0 + kr * P.row_step;
@@ -730,7 +732,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             const float u = 1.0f - sky_t;
             const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
             const f3 c = att * sky;
-            float* o = P.samples + ((size_t)fl * P.nrows * P.W + (size_t)kr * P.W + x) * 3u;
+            float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
@@ -773,16 +775,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 }
 
 // Folds P.nframes sample colours per pixel into the image, in frame order, with the same expression
-// k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per pixel; frame-major reads are
-// coalesced across the wave.
+// k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per tile-padded pixel, in the buffer's
+// tile-major order, so the frame-major colour reads are contiguous across the wave.
 __global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
-    const size_t npx = (size_t)P.nrows * P.W;
-    const size_t p = (size_t)blockIdx.x * 256u + threadIdx.x;
-    if (p >= npx) return;
-    float* px = P.image + p * 3u;
+    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
+    const size_t q = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (q >= npad) return;
+    const uint32_t tile = (uint32_t)(q >> 6), l = (uint32_t)(q & 63u);
+    const uint32_t x = (tile % P.tiles_w) * 8u + (l & 7u);
+    const uint32_t kr = (tile / P.tiles_w) * 8u + (l >> 3);
+    if (x >= P.W || kr >= P.nrows) return;
+    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
     float acc0 = px[0], acc1 = px[1], acc2 = px[2];
-    const float* c = P.samples + p * 3u;
-    for (uint32_t f = 0; f < P.nframes; f++, c += npx * 3u) {
+    const float* c = P.samples + q * 3u;
+    for (uint32_t f = 0; f < P.nframes; f++, c += npad * 3u) {
         const float fc = (float)(P.frame0 + f);
         const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
         const float omw = 1.0f - w;
@@ -837,9 +843,9 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
 
 // Sample queue, part 2: fold the chunk's colours into the image in frame order.
 hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
-    const size_t npx = (size_t)P.nrows * P.W;
-    if (npx == 0 || P.nframes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npx + 255u) / 256u)), dim3(256), 0, stream, P);
+    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
+    if (npad == 0 || P.nframes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npad + 255u) / 256u)), dim3(256), 0, stream, P);
     return hipGetLastError();
 }
 
