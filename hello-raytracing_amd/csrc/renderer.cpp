@@ -230,9 +230,13 @@ int trace_events(rt_renderer* r, uint32_t pair) {
     return RT_OK;
 }
 
-// schedule 0 = the sample queue (load-balanced at sample granularity).
-uint32_t resolve_schedule(const rt_renderer* r) {
-    return r->params.schedule ? r->params.schedule : RT_SCHEDULE_QUEUE;
+// schedule 0 = the sample queue (load-balanced at sample granularity), except for
+// draws too small to fill the persistent grid for long (< 4M samples: e.g. one interactive frame, C1),
+// where the tiles kernel's single launch has less fixed cost.
+uint32_t resolve_schedule(const rt_renderer* r, uint32_t count) {
+    if (r->params.schedule) return r->params.schedule;
+    const uint64_t samples = (uint64_t)count * r->local_rows() * r->width;
+    return samples < (4ull << 20) ? RT_SCHEDULE_TILES : RT_SCHEDULE_QUEUE;
 }
 
 int resolve_variant(const rt_renderer* r) {
@@ -311,7 +315,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.pad_k3 = 2e-3f;
     P.pad_k4 = 4.0f * u;
     const int variant = r->mode == RT_MODE_TRIS ? hrt_dev::SCAN_SIMPLE : resolve_variant(r);
-    const uint32_t schedule = resolve_schedule(r);
+    const uint32_t schedule = resolve_schedule(r, count);
     r->last_variant = variant;
     r->last_schedule = schedule;
 

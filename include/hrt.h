@@ -63,10 +63,11 @@ typedef struct rt_params {
     uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots up, else 3), 1 simple,
                                   3 packed + deferred exact candidates, 4 conservative culling BVH;
                                   all bit-identical. 2 and 5-10 were removed.    */
-    uint32_t schedule;         /* work schedule of rt_draw_frames: 0 auto, 1 tiles (one lane per pixel
-                                  for a launch's frames, in-register accumulation), 2 sample queue
-                                  (persistent grid pulling (pixel, frame) samples + in-order fold);
-                                  bit-identical                               */
+    uint32_t schedule;         /* work schedule of rt_draw / rt_draw_frames: 0 auto (queue from 4M
+                                  samples per draw, else tiles), 1 tiles (one lane per pixel for a
+                                  launch's frames, in-register accumulation), 2 sample queue (persistent
+                                  grid pulling 8x8-tile x job_frames jobs, colours folded in frame
+                                  order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 8        */
 } rt_params;

@@ -104,6 +104,21 @@ def test_sample_queue_equals_tiles(case):
         assert sb.schedule == hrt.RT_SCHEDULE_QUEUE and sb.samples == sa.samples
 
 
+def test_auto_schedule_by_draw_size():
+    """schedule 0 picks tiles below 4M samples per draw and the sample queue from there on."""
+    sd = scenes.golden_scene("shadow_rendering", 256, 256)
+    r = scenes.make_renderer(sd)
+    r.draw_frames(64, 1000, 10)  # 4 Mi samples
+    assert r.stats().schedule == hrt.RT_SCHEDULE_QUEUE
+    r.draw_frames(1, 2000, 10)
+    assert r.stats().schedule == hrt.RT_SCHEDULE_TILES
+    t = scenes.make_renderer(sd)
+    t.set_params(schedule=hrt.RT_SCHEDULE_TILES)
+    t.draw_frames(64, 1000, 10)
+    t.draw_frames(1, 2000, 10)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), t.read_image().view(np.uint32))
+
+
 def test_sample_queue_chunks_and_tris_mode():
     """Frame chunks bounded by the colour-buffer budget (1 and 2 frames per chunk at 320x240) and the
     triangle program under the queue schedule."""
