@@ -177,18 +177,44 @@ __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float
     return (-b - __builtin_sqrtf(disc)) / a2;
 }
 
+#ifndef HRT_SLAB_FMA
+#define HRT_SLAB_FMA 1
+#endif
+#ifndef HRT_SLAB_RCP
+#define HRT_SLAB_RCP 1
+#endif
+
+// 1/d for the slab tests, |d| >= 1e-30 (else +-1e30). v_rcp_f32 (1 ulp) by default: the padding budget
+// covers it (DESIGN.md §Sphere BVH exactness, slab arithmetic).
 __device__ __forceinline__ float robust_inv(float d) {
+#if HRT_SLAB_RCP
+    return __builtin_fabsf(d) >= 1e-30f ? __builtin_amdgcn_rcpf(d) : __builtin_copysignf(1e30f, d);
+#else
     return __builtin_fabsf(d) >= 1e-30f ? 1.0f / d : __builtin_copysignf(1e30f, d);
+#endif
 }
 
-// Slab test of the ray against a box padded by `pad` on every side (box relative to bvh_rc; lo/hi already
-// hold -o' -/+ pad). Visits when the padded box is entered before it is left, not behind the origin,
-// and not beyond the current best t (equality visits: ties must be seen).
-__device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx, const f3& lo, const f3& hi,
-                                               const f3& inv, float bt, float& tenter) {
-    const float t0x = (mn.x + lo.x) * inv.x, t1x = (mx.x + hi.x) * inv.x;
-    const float t0y = (mn.y + lo.y) * inv.y, t1y = (mx.y + hi.y) * inv.y;
-    const float t0z = (mn.z + lo.z) * inv.z, t1z = (mx.z + hi.z) * inv.z;
+// Per-query slab constants: the box bound b (relative to bvh_rc) enters as t = (b - o' -/+ pad) / d.
+struct Slab {
+    f3 inv;     // robust 1/d
+    f3 lo, hi;  // HRT_SLAB_FMA: (-o' - pad) * inv and (-o' + pad) * inv; else -o' - pad and -o' + pad
+};
+
+// Slab test of the ray against a box padded by `pad` on every side. Visits when the padded box is entered
+// before it is left, not behind the origin, and not beyond the current best t (equality visits: ties must
+// be seen). HRT_SLAB_FMA: one fma per plane, t = fma(b, inv, (-o' -/+ pad) * inv); its rounding error in
+// distance units is <= 3.02 u D (+1 u with v_rcp), inside the 1.02 delta >= 4.08 u D margin the padding leaves.
+__device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx, const Slab& S, float bt,
+                                               float& tenter) {
+#if HRT_SLAB_FMA
+    const float t0x = __builtin_fmaf(mn.x, S.inv.x, S.lo.x), t1x = __builtin_fmaf(mx.x, S.inv.x, S.hi.x);
+    const float t0y = __builtin_fmaf(mn.y, S.inv.y, S.lo.y), t1y = __builtin_fmaf(mx.y, S.inv.y, S.hi.y);
+    const float t0z = __builtin_fmaf(mn.z, S.inv.z, S.lo.z), t1z = __builtin_fmaf(mx.z, S.inv.z, S.hi.z);
+#else
+    const float t0x = (mn.x + S.lo.x) * S.inv.x, t1x = (mx.x + S.hi.x) * S.inv.x;
+    const float t0y = (mn.y + S.lo.y) * S.inv.y, t1y = (mx.y + S.hi.y) * S.inv.y;
+    const float t0z = (mn.z + S.lo.z) * S.inv.z, t1z = (mx.z + S.hi.z) * S.inv.z;
+#endif
     const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmax_ieee(fmin_ieee(t0z, t1z), 0.0f));
     const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmin_ieee(fmax_ieee(t0z, t1z), bt));
     tenter = tmin;
@@ -226,9 +252,14 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     const float dn = __builtin_amdgcn_sqrtf(a);
     const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
     const float pad = 2.02f * delta;
-    const f3 inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
-    const f3 lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-    const f3 hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+    Slab S;
+    S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+#if HRT_SLAB_FMA
+    S.lo = S.lo * S.inv;
+    S.hi = S.hi * S.inv;
+#endif
 
     const float4* __restrict__ nodes = P.bvh_nodes;
     uint32_t node = P.bvh_root;
@@ -241,8 +272,8 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             const float4 n2 = nodes[4 * node + 2];
             const float4 n3 = nodes[4 * node + 3];
             float tl, tr;
-            const bool hl = padded_box_hit(n0, n1, lo, hi, inv, bt, tl);
-            const bool hr = padded_box_hit(n2, n3, lo, hi, inv, bt, tr);
+            const bool hl = padded_box_hit(n0, n1, S, bt, tl);
+            const bool hr = padded_box_hit(n2, n3, S, bt, tr);
             tally.boxes += 2;
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
             if (hl && hr) {
