@@ -305,6 +305,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.bvh_slot = r->bvh_slot.ptr;
     P.large_slots = r->bvh_large.ptr;
     P.nlarge = (uint32_t)B.large.size();
+    P.bvh_nleaf = (uint32_t)B.slot.size();
     P.bvh_root = B.root_word;
     for (int k = 0; k < 3; k++) P.bvh_rc[k] = B.root_center[k];
     P.bvh_rr = B.root_radius;

@@ -87,6 +87,7 @@ struct KParams {
     const int* bvh_slot;          // original slot of each leaf sphere
     const int* large_slots;       // slots scanned linearly for every ray
     uint32_t nlarge, bvh_root;    // large-list length, root child word
+    uint32_t bvh_nleaf, pad_l;    // spheres in the BVH (bvh_sph / bvh_slot entries)
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     const float4* nodes;          // 2 float4 per node: min, max

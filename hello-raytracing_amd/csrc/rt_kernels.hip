@@ -236,12 +236,18 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
         tally.spheres += P.nslots;
         return scan_spheres(P, r, best);
     }
+    // The running winner is kept as a code: BVH-order position (< nleaf) or nleaf + large-list index, so
+    // a leaf test needs no slot load; slots are fetched only to break an exact t tie and at the end.
+    const uint32_t nleaf = P.bvh_nleaf;
+    auto slot_of = [&](int code) -> int {
+        return (uint32_t)code < nleaf ? P.bvh_slot[code] : P.large_slots[code - (int)nleaf];
+    };
     float bt = best;
-    int bi = -1;
-    for (uint32_t k = 0; k < P.nlarge; k++) {
+    int bc = -1;
+    for (uint32_t k = 0; k < P.nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
         const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
-        if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+        if (beats(t, i, bt, bc >= 0 ? slot_of(bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
     tally.spheres += P.nlarge;
 
@@ -293,8 +299,9 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
             for (uint32_t j = 0; j < cnt; j++) {
                 const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
-                const int i = P.bvh_slot[first + j];
-                if (beats(t, i, bt, bi)) { bt = t; bi = i; }
+                if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
+                    if (t < bt || (bc >= 0 && P.bvh_slot[first + j] < slot_of(bc))) { bt = t; bc = (int)(first + j); }
+                }
             }
             tally.spheres += cnt;
         }
@@ -306,7 +313,7 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
         return scan_spheres(P, r, best);
     }
     best = bt;
-    return bi;
+    return bc >= 0 ? slot_of(bc) : -1;
 }
 
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
