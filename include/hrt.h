@@ -60,7 +60,7 @@ typedef struct rt_params {
     uint32_t min_sphere_slots; /* arrayLength(&scene) floor; default 100 (zero-filled slots traced)    */
     uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
-    uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots up, else 3), 1 simple,
+    uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots, 3 from 9, else 1), 1 simple,
                                   3 packed + deferred exact candidates, 4 conservative culling BVH;
                                   all bit-identical. 2 and 5-10 were removed.    */
     uint32_t schedule;         /* work schedule of rt_draw / rt_draw_frames: 0 auto (queue from 4M
