@@ -369,11 +369,22 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
 }
 
 // intersect_all_node (shader_tris.wgsl:268-301): stackless DFS over the implicit heap, 600-step cap.
-__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h, Tally& tally) {
+// The walk's path never depends on hits (intersect_node has no best-t test), so the triangle tests of
+// the leaves it reaches are deferred into a per-lane list (`cand`, LDS, stride 256) and run in batches:
+// whenever some lane's list is full, every active lane tests its pending triangles, in the order reached
+// (= the reference's sequential `t >= best` rule, so the same winner). The walk loop then carries only
+// node tests, and triangle tests run with most lanes active instead of one divergent branch per step.
+constexpr uint32_t TRI_BATCH = 8;
+
+__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h, Tally& tally, uint32_t* cand) {
     const f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const uint32_t n = P.n, m = P.m;
-    uint32_t i = 1;
+    uint32_t i = 1, nc = 0;
     for (int step = 0; step < 600; step++) {
+        if (__ballot(nc == TRI_BATCH) != 0ull) {
+            for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], h);
+            nc = 0;
+        }
         if (i < n) {
             tally.nodes++;
             if (node_hit(P, i, r.o, inv)) {
@@ -385,16 +396,18 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h,
             const uint32_t j = i - n;
             if (j >= m) break;
             tally.tris++;
-            tri_test(P, r, j, h);
+            cand[(nc++) * 256u] = j;
         }
         i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
         if (i == 0u) break;
         i++;
     }
+    for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], h);
 }
 
 template <int MODE, int SCAN>
-__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally) {
+__device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally,
+                                            uint32_t* tri_cand) {
     h.t = FLT_MAX_REF;
     if (MODE != MODE_TRIS) {
         float best = FLT_MAX_REF;
@@ -410,7 +423,7 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
         }
         if (bi >= 0) sphere_record(P, r, bi, best, h);
     }
-    if (MODE != MODE_SPHERE) walk_bvh(P, r, h, tally);
+    if (MODE != MODE_SPHERE) walk_bvh(P, r, h, tally, tri_cand);
     // abs(hit.t - FLT_MAX) < EPSILON (shader_sphere.wgsl:235): t is FLT_MAX_REF exactly or >= 2^103 away.
     return h.t != FLT_MAX_REF;
 }
@@ -508,12 +521,21 @@ template <int MODE, int SCAN>
 __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* lds_list = nullptr;
+    uint32_t* tri_cand = nullptr;  // triangle program: deferred triangle list (aliases the sphere scan's
+                                   // LDS list, which is free again once the sphere scan has returned)
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
+        static_assert((CAND_CAP + 1) * 2 >= TRI_BATCH * 4, "tri list alias");
         lds_list = cand + threadIdx.x;
+        tri_cand = (uint32_t*)cand + threadIdx.x;
     } else if constexpr (SCAN == SCAN_BVH) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+        static_assert(BVH_STACK >= (int)TRI_BATCH, "tri list alias");
         lds_list = bvh_stack + threadIdx.x;
+        tri_cand = bvh_stack + threadIdx.x;
+    } else if constexpr (MODE != MODE_SPHERE) {
+        __shared__ uint32_t tri_list[TRI_BATCH * 256];
+        tri_cand = tri_list + threadIdx.x;
     }
     Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
@@ -553,7 +575,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 #endif
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, tri_cand);
             queries++;
 #ifdef HRT_STAMPS
             st_tb = hrt_stamp();
@@ -670,12 +692,21 @@ template <int MODE, int SCAN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     void* lds_list = nullptr;
+    uint32_t* tri_cand = nullptr;  // triangle program: deferred triangle list (aliases the sphere scan's
+                                   // LDS list, which is free again once the sphere scan has returned)
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
+        static_assert((CAND_CAP + 1) * 2 >= TRI_BATCH * 4, "tri list alias");
         lds_list = cand + threadIdx.x;
+        tri_cand = (uint32_t*)cand + threadIdx.x;
     } else if constexpr (SCAN == SCAN_BVH) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+        static_assert(BVH_STACK >= (int)TRI_BATCH, "tri list alias");
         lds_list = bvh_stack + threadIdx.x;
+        tri_cand = bvh_stack + threadIdx.x;
+    } else if constexpr (MODE != MODE_SPHERE) {
+        __shared__ uint32_t tri_list[TRI_BATCH * 256];
+        tri_cand = tri_list + threadIdx.x;
     }
     Tally tally;
     uint32_t queries = 0;
@@ -751,7 +782,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally);
+            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, tri_cand);
             queries++;
 #ifdef HRT_STAMPS
             st_ta = hrt_stamp();
