@@ -338,17 +338,20 @@ def test_small_tris_scenes_vs_oracle(builder):
     assert_parity(scene.renderer.read_image(), ref, builder)
 
 
-def test_mixed_mode_suzanne_ground_vs_oracle():
+@pytest.mark.parametrize("schedule", [1, 2])
+@pytest.mark.parametrize("variant", [1, 3, 4])
+def test_mixed_mode_suzanne_ground_vs_oracle(variant, schedule):
     sd = scenes.config_c4(96, 54, 4)
-    r = scenes.make_renderer(sd)
-    r.draw_frames(sd.frames, 1000, 10)
     ref, q = scenes.oracle_render(sd)
     from oracle import oracle as O
-    assert_parity(r.read_image(), ref, "C4 mixed 96x54")
+    r = scenes.make_renderer(sd)
+    r.set_params(variant=variant, schedule=schedule)
+    r.draw_frames(sd.frames, 1000, 10)
+    assert_parity(r.read_image(), ref, f"C4 mixed 96x54 variant {variant} schedule {schedule}")
     st = r.stats()
     # the reference's implicit-heap walk, step for step: identical node and triangle test counts
     assert st.queries == q and st.node_tests == O.last_counts["node_tests"] and st.tri_tests == O.last_counts["tri_tests"]
-    assert st.node_tests > 0 and st.tri_tests > 0
+    assert st.node_tests > 0 and st.tri_tests > 0 and st.variant == variant and st.schedule == schedule
 
 
 def test_large_frame_count_ema_regime():
