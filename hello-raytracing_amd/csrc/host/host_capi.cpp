@@ -65,6 +65,12 @@ int rt_host_tree_build(rt_tree* t) {
     return RT_OK;
 }
 
+int rt_host_tree_build_threads(rt_tree* t, int threads) {
+    if (!t || threads < 0) return RT_ERR_ARG;
+    t->tree.build((unsigned)threads);
+    return RT_OK;
+}
+
 int rt_host_tree_view(const rt_tree* t, uint32_t sizes[2], const void** nodes32, uint32_t* n_nodes,
                       const void** tris64, uint32_t* n_tris, const void** mats32, uint32_t* n_mats) {
     if (!t) return RT_ERR_ARG;

@@ -6,7 +6,11 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <deque>
+#include <thread>
+#include <cstdlib>
+#include <iterator>
 #include <sstream>
 #include <tuple>
 
@@ -81,38 +85,154 @@ static size_t next_power_of_two(size_t v) {
     return n;
 }
 
-void Tree::build() {
+namespace {
+
+// Stable sort of (key, index) pairs by key, `a.first < b.first` (NaN never less: partial_cmp Equal).
+// Without NaN keys it is an LSD radix sort on an order-preserving u32 image of the key (+0 and -0 mapped
+// together, as `<` treats them as equal), which equals std::stable_sort element for element; any NaN key
+// falls back to std::stable_sort itself.
+void stable_sort_pairs(std::vector<std::pair<float, uint32_t>>& v, std::vector<std::pair<uint32_t, uint32_t>>& a,
+                       std::vector<std::pair<uint32_t, uint32_t>>& b) {
+    const size_t len = v.size();
+    bool nan = false;
+    for (const auto& p : v) nan |= std::isnan(p.first);
+    if (len < 512 || nan) {
+        std::stable_sort(v.begin(), v.end(), [](const std::pair<float, uint32_t>& x, const std::pair<float, uint32_t>& y) {
+            return x.first < y.first;
+        });
+        return;
+    }
+    a.resize(len);
+    b.resize(len);
+    for (size_t k = 0; k < len; k++) {
+        const float f = v[k].first == 0.0f ? 0.0f : v[k].first;
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        a[k] = {(u & 0x80000000u) ? ~u : (u | 0x80000000u), v[k].second};
+    }
+    for (int shift = 0; shift < 32; shift += 8) {
+        size_t count[257] = {0};
+        for (size_t k = 0; k < len; k++) count[((a[k].first >> shift) & 255u) + 1]++;
+        if (count[((a[0].first >> shift) & 255u) + 1] == len) continue;  // one bucket: pass is a no-op
+        for (int d = 0; d < 256; d++) count[d + 1] += count[d];
+        for (size_t k = 0; k < len; k++) b[count[(a[k].first >> shift) & 255u]++] = a[k];
+        a.swap(b);
+    }
+    for (size_t k = 0; k < len; k++) v[k].second = a[k].second;  // keys are not needed after the sort
+}
+
+unsigned default_threads() {
+    if (const char* e = std::getenv("HRT_HOST_THREADS")) return (unsigned)std::max(1, std::atoi(e));
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+}  // namespace
+
+void Tree::build(unsigned threads) {
     // tree.rs:36-56: BFS over the padded power-of-two index space; stable sort of each range by the
     // centroid coordinate of axis depth % 3 (partial_cmp, NaN = Equal), split at the index midpoint.
+    // Here the sorts permute a u32 index array (the 64-byte triangles move once, at the end), and a range
+    // only needs its parent's sort to have happened first, so once the top levels have produced one range
+    // per thread, each thread finishes whole subtrees on its own. A stable sort's output is unique for
+    // the comparator, so the tree is byte-identical to the sequential BFS for any thread count.
+    if (threads == 0) threads = default_threads();
     const size_t m = triangles.size();
     const size_t n = next_power_of_two(m);
-    std::deque<std::tuple<size_t, size_t, size_t>> q;
-    q.emplace_back(0, n, 0);
-    while (!q.empty()) {
-        auto [i, j, depth] = q.front();
-        q.pop_front();
-        size_t l = i, r = std::min(j, m);
-        if (l + 1 >= r) continue;
-        const int axis = (int)(depth % 3);
-        std::stable_sort(triangles.begin() + l, triangles.begin() + r, [axis](const Triangle& a, const Triangle& b) {
-            const float* ca = &a.custom.x;
-            const float* cb = &b.custom.x;
-            return ca[axis] < cb[axis];
-        });
-        size_t mid = (i + j) / 2;
-        q.emplace_back(i, mid, depth + 1);
-        q.emplace_back(mid, j, depth + 1);
+    std::vector<uint32_t> perm(m);
+    for (size_t k = 0; k < m; k++) perm[k] = (uint32_t)k;
+    const float* key = &triangles.data()->custom.x;  // custom of triangle k at key[k * 16 + axis]
+    static_assert(sizeof(Triangle) == 64, "Triangle stride");
+    // sort (key, index) pairs in a per-thread buffer: contiguous keys instead of one gather per compare
+    using Pairs = std::vector<std::pair<float, uint32_t>>;
+    using Keys = std::vector<std::pair<uint32_t, uint32_t>>;
+    auto sort_range = [&](size_t i, size_t j, size_t depth, Pairs& tmp, Keys& ra, Keys& rb) -> bool {
+        const size_t l = i, r = std::min(j, m);  // false: the range is not split further
+        if (l + 1 >= r) return false;
+        const size_t axis = depth % 3;
+        tmp.resize(r - l);
+        for (size_t k = l; k < r; k++) tmp[k - l] = {key[(size_t)perm[k] * 16u + axis], perm[k]};
+        stable_sort_pairs(tmp, ra, rb);
+        for (size_t k = l; k < r; k++) perm[k] = tmp[k - l].second;
+        return true;
+    };
+    struct Range {
+        size_t i, j, depth;
+    };
+    std::vector<Range> level{{0, n, 0}};
+    Pairs tmp0;
+    Keys ra0, rb0;
+    while (!level.empty() && level.size() < threads) {  // top levels, sequentially
+        std::vector<Range> next;
+        for (const Range& g : level)
+            if (sort_range(g.i, g.j, g.depth, tmp0, ra0, rb0)) {
+                const size_t mid = (g.i + g.j) / 2;
+                next.push_back({g.i, mid, g.depth + 1});
+                next.push_back({mid, g.j, g.depth + 1});
+            }
+        level.swap(next);
     }
-    // tree.rs:57-65: leaf i is heap node i + n; every ancestor's box is the union of its vertices.
+    auto subtrees = [&](size_t first, size_t step) {  // whole subtrees, depth first
+        std::vector<Range> stack;
+        Pairs tmp;
+        Keys ra, rb;
+        for (size_t k = first; k < level.size(); k += step) {
+            stack.push_back(level[k]);
+            while (!stack.empty()) {
+                const Range g = stack.back();
+                stack.pop_back();
+                if (!sort_range(g.i, g.j, g.depth, tmp, ra, rb)) continue;
+                const size_t mid = (g.i + g.j) / 2;
+                stack.push_back({mid, g.j, g.depth + 1});
+                stack.push_back({g.i, mid, g.depth + 1});
+            }
+        }
+    };
+    if (threads > 1 && level.size() > 1) {
+        std::vector<std::thread> pool;
+        for (unsigned t = 0; t < threads; t++) pool.emplace_back(subtrees, (size_t)t, (size_t)threads);
+        for (auto& t : pool) t.join();
+    } else {
+        subtrees(0, 1);
+    }
+    std::vector<Triangle> sorted(m);
+    for (size_t k = 0; k < m; k++) sorted[k] = triangles[perm[k]];
+    triangles.swap(sorted);
+    // tree.rs:57-65: leaf i is heap node i + n; every ancestor's box is the union of its vertices, united
+    // triangle by triangle in index order. Without NaN coordinates that fold equals a bottom-up merge:
+    // SSE min/max keep the LAST element equal to the extremum, and min(fold(L), fold(R)) picks exactly
+    // that element of L ++ R (also for +-0). NaN makes the fold order-dependent: then the literal loop.
     nodes.assign(n, Node::empty());
-    for (size_t i = 0; i < m; i++) {
-        const Triangle& t = triangles[i];
-        size_t j = (i + n) / 2;
-        while (j > 0) {
-            nodes[j].unite(t.a);
-            nodes[j].unite(t.b);
-            nodes[j].unite(t.c);
-            j /= 2;
+    bool has_nan = false;
+    for (const Triangle& t : triangles)
+        for (const Vec4* v : {&t.a, &t.b, &t.c})
+            has_nan |= std::isnan(v->x) || std::isnan(v->y) || std::isnan(v->z) || std::isnan(v->w);
+    if (!has_nan) {
+        for (size_t j = n / 2; j < n; j++)  // parents of leaves 2j, 2j + 1
+            for (size_t c = 2 * j; c <= 2 * j + 1; c++)
+                if (c - n < m) {
+                    const Triangle& t = triangles[c - n];
+                    nodes[j].unite(t.a);
+                    nodes[j].unite(t.b);
+                    nodes[j].unite(t.c);
+                }
+        for (size_t j = n / 2; j-- > 1;) {
+            const Node& l = nodes[2 * j];
+            const Node& r = nodes[2 * j + 1];
+            nodes[j].bound_min = {sse_min(l.bound_min.x, r.bound_min.x), sse_min(l.bound_min.y, r.bound_min.y),
+                                  sse_min(l.bound_min.z, r.bound_min.z), sse_min(l.bound_min.w, r.bound_min.w)};
+            nodes[j].bound_max = {sse_max(l.bound_max.x, r.bound_max.x), sse_max(l.bound_max.y, r.bound_max.y),
+                                  sse_max(l.bound_max.z, r.bound_max.z), sse_max(l.bound_max.w, r.bound_max.w)};
+        }
+    } else {
+        for (size_t i = 0; i < m; i++) {
+            const Triangle& t = triangles[i];
+            size_t j = (i + n) / 2;
+            while (j > 0) {
+                nodes[j].unite(t.a);
+                nodes[j].unite(t.b);
+                nodes[j].unite(t.c);
+                j /= 2;
+            }
         }
     }
     // tree.rs:66-70: custom := unit geometric normal.

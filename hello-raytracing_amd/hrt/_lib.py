@@ -100,6 +100,7 @@ SIGNATURES = {
     "rt_host_tree_new": (C.c_int, [C.POINTER(_P)]),
     "rt_host_tree_add_mesh": (C.c_int, [_P, _P]),
     "rt_host_tree_build": (C.c_int, [_P]),
+    "rt_host_tree_build_threads": (C.c_int, [_P, C.c_int]),
     "rt_host_tree_view": (
         C.c_int,
         [_P, _PU32, C.POINTER(_P), _PU32, C.POINTER(_P), _PU32, C.POINTER(_P), _PU32],

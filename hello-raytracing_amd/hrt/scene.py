@@ -178,8 +178,12 @@ class Tree:
     def add_mesh(self, mesh: Mesh) -> None:
         check(lib().rt_host_tree_add_mesh(self._h, mesh._h), "Tree::add_mesh")
 
-    def build(self) -> None:
-        check(lib().rt_host_tree_build(self._h), "Tree::build")
+    def build(self, threads: int = 0) -> None:
+        """tree.rs:36-72. threads 0 = all (capped at 16); the result does not depend on it."""
+        if threads:
+            check(lib().rt_host_tree_build_threads(self._h, threads), "Tree::build")
+        else:
+            check(lib().rt_host_tree_build(self._h), "Tree::build")
 
     def view(self):
         """(sizes[2], nodes, triangles, materials) as numpy copies."""
@@ -435,6 +439,27 @@ class SceneTris:
     def new_suzane(width: int, height: int) -> "SceneTris":
         return SceneTris(Renderer(width, height, RT_MODE_TRIS), SceneTris.suzane_camera(),
                          SceneTris.build_suzane_tree())
+
+    @staticmethod
+    def _mesh_on_floor(asset: str, albedo: Vec3) -> Tree:
+        tree = Tree.from_mesh(Mesh.load_obj(read_asset(asset), Material.new_lambertian(albedo)))
+        tree.add_mesh(Mesh.load_obj(read_asset("floor.obj"), Material.new_lambertian(Vec3(0.5, 0.5, 0.6))))
+        tree.build()
+        return tree
+
+    @staticmethod
+    def new_dragon(width: int, height: int) -> "SceneTris":
+        """scene_tris.rs:67-92 (xyzrgb_dragon_lp_20.obj + floor.obj, 49,988 triangles)."""
+        tree = SceneTris._mesh_on_floor("xyzrgb_dragon_lp_20.obj", Vec3(0.7, 0.7, 0.2))
+        camera = Camera.new(Vec3(0.0, 2.0, 8.0), Vec3(0.0, 0.0, -8.0), 5.6, 0.0, PI * f32(0.3))
+        return SceneTris(Renderer(width, height, RT_MODE_TRIS), camera, tree)
+
+    @staticmethod
+    def new_lucy(width: int, height: int) -> "SceneTris":
+        """scene_tris.rs:93-118 (lucy_lp_20.obj + floor.obj)."""
+        tree = SceneTris._mesh_on_floor("lucy_lp_20.obj", Vec3(0.4, 0.3, 0.6))
+        camera = Camera.new(Vec3(0.0, 5.0, 6.0), Vec3(0.0, 0.0, -8.0), 5.6, 0.0, PI * f32(0.3))
+        return SceneTris(Renderer(width, height, RT_MODE_TRIS), camera, tree)
 
     @staticmethod
     def new_cube(width: int, height: int) -> "SceneTris":

@@ -174,6 +174,9 @@ int rt_host_mesh_destroy(rt_mesh *m);
 int rt_host_tree_new(rt_tree **out);
 int rt_host_tree_add_mesh(rt_tree *t, const rt_mesh *m);
 int rt_host_tree_build(rt_tree *t);
+/* Tree::build on `threads` host threads (0 = HRT_HOST_THREADS or min(16, cores); rt_host_tree_build uses 0).
+ * Level-synchronous BFS with concurrent stable sorts: byte-identical to the sequential build. */
+int rt_host_tree_build_threads(rt_tree *t, int threads);
 /* Views into the tree (valid until the next mutation): sizes [n, m], n nodes, m triangles, k materials. */
 int rt_host_tree_view(const rt_tree *t, uint32_t sizes[2], const void **nodes32, uint32_t *n_nodes,
                       const void **tris64, uint32_t *n_tris, const void **mats32, uint32_t *n_mats);

@@ -328,6 +328,26 @@ def test_suzanne_tris_mode_vs_oracle():
     assert_parity(img, ref, "new_suzane tris")
 
 
+@pytest.mark.parametrize("builder", ["new_dragon", "new_lucy"])
+def test_large_mesh_scenes_vs_oracle(builder):
+    """scene_tris.rs:67-118: 50k / 20k-triangle heaps (n = 65536 / 32768), deep walks near the 600-step cap."""
+    scene = getattr(hrt.SceneTris, builder)(64, 48)
+    scene.init()
+    for i in range(3):
+        scene.set_time(1000 + 10 * i)
+        scene.draw()
+    sd = scenes.SceneDef(builder, hrt.RT_MODE_TRIS, 64, 48, scene.camera, bvh=scene.tris_bvh.view(), frames=3)
+    ref, q = scenes.oracle_render(sd)
+    from oracle import oracle as O
+    assert_parity(scene.renderer.read_image(), ref, builder)
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, job_frames=1)
+    r.draw_frames(3, 1000, 10)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), scene.renderer.read_image().view(np.uint32))
+    st = r.stats()
+    assert st.queries == q and st.node_tests == O.last_counts["node_tests"] and st.tri_tests == O.last_counts["tri_tests"]
+
+
 @pytest.mark.parametrize("builder", ["new_cube", "new_quad"])
 def test_small_tris_scenes_vs_oracle(builder):
     scene = getattr(hrt.SceneTris, builder)(64, 48)

@@ -84,6 +84,21 @@ def test_tree_build_lucy_matches_restatement():
     _tree_bytes_match([("lucy_lp_20.obj", LAMB), ("floor.obj", LAMB)])
 
 
+def test_parallel_tree_build_is_byte_identical():
+    """SURVEY 8(f) 2: the level-synchronous multi-threaded Tree::build equals the sequential one byte for
+    byte (dragon: 49,988 triangles, n = 65536; lucy) for several thread counts."""
+    for asset in ("xyzrgb_dragon_lp_20.obj", "lucy_lp_20.obj"):
+        views = []
+        for threads in (1, 3, 8, 16):
+            t = Tree.from_mesh(Mesh.load_obj(hrt.read_asset(asset), LAMB))
+            t.add_mesh(Mesh.load_obj(hrt.read_asset("floor.obj"), LAMB))
+            t.build(threads=threads)
+            sizes, nodes, tris, mats = t.view()
+            views.append((sizes, nodes.tobytes(), tris.tobytes(), mats.tobytes()))
+        assert all(v == views[0] for v in views[1:]), asset
+    assert views[0][0] == [32768, 19929]  # lucy
+
+
 # ---- OBJ edge cases (tobj behaviour the reference relies on)
 def test_obj_negative_indices_models_and_quads():
     src = b"""o A
