@@ -76,6 +76,8 @@ def main() -> int:
     ap.add_argument("--frames-per-launch", type=int, default=1024, help="tiles schedule: frames per launch")
     ap.add_argument("--schedule", type=int, default=0, help="0 auto (queue), 1 tiles, 2 sample queue")
     ap.add_argument("--job-frames", type=int, default=8, help="sample queue: frames per 8x8-tile job")
+    ap.add_argument("--tri-bvh", type=int, default=0,
+                    help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
                     help="sphere-scan kernel: 0 auto, 1 simple, 2 packed, 3 deferred, 4 culling BVH")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -121,7 +123,7 @@ def main() -> int:
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
     r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
-                 schedule=args.schedule, job_frames=args.job_frames)
+                 schedule=args.schedule, job_frames=args.job_frames, tri_bvh=args.tri_bvh)
     local_rows = r.local_rows
     max_rows = (sd.height + world - 1) // world
     part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
@@ -282,7 +284,7 @@ def main() -> int:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)
             ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
-                             job_frames=args.job_frames)
+                             job_frames=args.job_frames, tri_bvh=args.tri_bvh)
             ref_r.draw_frames(sd.frames, 1000, 10)
             ref_img = torch.from_numpy(ref_r.read_image())
             same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))

@@ -1,0 +1,198 @@
+// tri_bvh.cpp — binned-SAH BVH2 over triangles for the opt-in triangle walk (tri_bvh.hpp).
+#include "tri_bvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+
+namespace hrt {
+namespace {
+
+struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY};
+    double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    void grow(const double p[3]) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    double area() const {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0 && dy >= 0 && dz >= 0)) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+// f32 bounds that contain the double value, with one extra ulp outward
+float down(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -INFINITY);
+    return std::nextafter(f, -INFINITY);
+}
+float up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return std::nextafter(f, INFINITY);
+}
+
+struct Prim {
+    Box box;
+    double cen[3];
+    uint32_t index;
+};
+
+constexpr uint32_t MAX_LEAF = 4;
+constexpr int BINS = 16;
+
+struct Builder {
+    std::vector<Prim> prims;
+    TriBvh* out;
+    uint32_t max_depth = 0;
+
+    uint32_t leaf(size_t first, size_t count) {
+        const uint32_t f = (uint32_t)out->order.size();
+        for (size_t i = first; i < first + count; i++) out->order.push_back(prims[i].index);
+        return BVH_LEAF_BIT | (f << 4) | (uint32_t)count;
+    }
+
+    uint32_t build(size_t first, size_t count, uint32_t depth, Box* bounds) {
+        Box b;
+        for (size_t i = first; i < first + count; i++) b.grow(prims[i].box);
+        *bounds = b;
+        max_depth = std::max(max_depth, depth);
+        if (count <= 1) return leaf(first, count);
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t i = first; i < first + count; i++)
+            for (int k = 0; k < 3; k++) {
+                clo[k] = std::min(clo[k], prims[i].cen[k]);
+                chi[k] = std::max(chi[k], prims[i].cen[k]);
+            }
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        const double ext = chi[axis] - clo[axis];
+        size_t mid = first + count / 2;
+        bool median = depth >= 48 || !(ext > 0.0);
+        if (!median) {
+            Box bb[BINS];
+            size_t bc[BINS] = {0};
+            auto bin_of = [&](const Prim& p) {
+                const int i = (int)((p.cen[axis] - clo[axis]) / ext * BINS);
+                return std::min(BINS - 1, std::max(0, i));
+            };
+            for (size_t i = first; i < first + count; i++) {
+                const int k = bin_of(prims[i]);
+                bb[k].grow(prims[i].box);
+                bc[k]++;
+            }
+            // sweep: right-side boxes from the top, then the left side incrementally
+            Box rb[BINS];
+            size_t rc[BINS] = {0};
+            Box acc;
+            size_t nacc = 0;
+            for (int k = BINS - 1; k >= 1; k--) {
+                acc.grow(bb[k]);
+                nacc += bc[k];
+                rb[k] = acc;
+                rc[k] = nacc;
+            }
+            double best = std::numeric_limits<double>::infinity();
+            int best_k = -1;
+            Box lacc;
+            size_t nl = 0;
+            for (int k = 1; k < BINS; k++) {
+                lacc.grow(bb[k - 1]);
+                nl += bc[k - 1];
+                if (!nl || !rc[k]) continue;
+                const double cost = lacc.area() * (double)nl + rb[k].area() * (double)rc[k];
+                if (cost < best) {
+                    best = cost;
+                    best_k = k;
+                }
+            }
+            // leaf when splitting does not pay (1 = relative cost of a box test vs a triangle test)
+            if (count <= MAX_LEAF && !(1.0 * b.area() + best < b.area() * (double)count)) return leaf(first, count);
+            if (best_k < 0) {
+                median = true;
+            } else {
+                auto it = std::partition(prims.begin() + (long)first, prims.begin() + (long)(first + count),
+                                         [&](const Prim& p) { return bin_of(p) < best_k; });
+                mid = (size_t)(it - prims.begin());
+                if (mid == first || mid == first + count) median = true;
+            }
+        }
+        if (median) {
+            if (count <= MAX_LEAF) return leaf(first, count);
+            std::nth_element(prims.begin() + (long)first, prims.begin() + (long)(first + count / 2),
+                             prims.begin() + (long)(first + count),
+                             [&](const Prim& a, const Prim& c) { return a.cen[axis] < c.cen[axis]; });
+            mid = first + count / 2;
+        }
+        const uint32_t idx = (uint32_t)out->nodes.size();
+        out->nodes.push_back(SphereBvhNode{});
+        Box lb, rbx;
+        const uint32_t lw = build(first, mid - first, depth + 1, &lb);
+        const uint32_t rw = build(mid, first + count - mid, depth + 1, &rbx);
+        SphereBvhNode& n = out->nodes[idx];
+        for (int k = 0; k < 3; k++) {
+            n.lmin[k] = down(lb.lo[k]);
+            n.lmax[k] = up(lb.hi[k]);
+            n.rmin[k] = down(rbx.lo[k]);
+            n.rmax[k] = up(rbx.hi[k]);
+        }
+        n.left = lw;
+        n.right = rw;
+        return idx;
+    }
+};
+
+}  // namespace
+
+TriBvh build_tri_bvh(const std::vector<float>& aee) {
+    TriBvh out;
+    const size_t m = aee.size() / 9;
+    Builder b;
+    b.out = &out;
+    b.prims.reserve(m);
+    for (size_t j = 0; j < m; j++) {
+        const float* t = &aee[9 * j];
+        Prim p;
+        double v[3][3];
+        for (int k = 0; k < 3; k++) {
+            v[0][k] = t[k];
+            v[1][k] = (double)t[k] + (double)t[3 + k];  // exact in double
+            v[2][k] = (double)t[k] + (double)t[6 + k];
+        }
+        bool finite = true;
+        for (int q = 0; q < 3; q++)
+            for (int k = 0; k < 3; k++) finite &= std::isfinite(v[q][k]);
+        if (!finite) continue;  // never accepted by Moller-Trumbore's finite-t tests in practice (non-parity mode)
+        for (int q = 0; q < 3; q++) p.box.grow(v[q]);
+        for (int k = 0; k < 3; k++) p.cen[k] = (v[0][k] + v[1][k] + v[2][k]) / 3.0;
+        p.index = (uint32_t)j;
+        b.prims.push_back(p);
+    }
+    Box root;
+    out.root_word = b.build(0, b.prims.size(), 0, &root);
+    out.depth = b.max_depth;
+    if (!b.prims.empty()) {
+        double diag2 = 0.0;
+        for (int k = 0; k < 3; k++) {
+            const double c = 0.5 * (root.lo[k] + root.hi[k]);
+            out.root_center[k] = (float)c;
+            const double h = std::max(root.hi[k] - (double)out.root_center[k], (double)out.root_center[k] - root.lo[k]);
+            diag2 += h * h;
+        }
+        out.root_radius = up(std::sqrt(diag2) * (1.0 + 1e-6));
+    }
+    return out;
+}
+
+}  // namespace hrt

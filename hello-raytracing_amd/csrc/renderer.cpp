@@ -17,6 +17,7 @@
 #include "../../include/hrt.h"
 #include "host/scene.hpp"
 #include "host/sphere_bvh.hpp"
+#include "host/tri_bvh.hpp"
 #include "rt_device.hpp"
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
@@ -110,6 +111,12 @@ struct rt_renderer {
     DevBuf<hrt_dev::TriDev> tris;
     DevBuf<hrt_dev::MatDev> mats;
     uint32_t bvh_n = 0, bvh_m = 0;
+    // opt-in SAH triangle tree, built on first use after rt_set_bvh
+    std::vector<float> tri_aee;  // a, e1, e2 of every triangle as uploaded
+    bool tri_tree_dirty = true;
+    hrt::TriBvh tri_tree;
+    DevBuf<float4> tb_nodes;
+    DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
     DevBuf<float> samples;  // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
@@ -136,6 +143,40 @@ int zero_image(rt_renderer* r) {
     int rc = ensure(r->image, r->image_floats());
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(r->image.ptr, 0, std::max<size_t>(r->image_floats(), 1) * sizeof(float), r->stream));
+    return RT_OK;
+}
+
+// Nodes of a two-child BVH as the kernels read them: 4 float4 per node, boxes relative to `center`,
+// rounded outward again after the shift.
+std::vector<float4> pack_bvh_nodes(const std::vector<hrt::SphereBvhNode>& nodes, const float center[3]) {
+    std::vector<float4> out(4 * std::max<size_t>(nodes.size(), 1));
+    auto rel_lo = [&](float v, int k) { return std::nextafter((float)((double)v - (double)center[k]), -INFINITY); };
+    auto rel_hi = [&](float v, int k) { return std::nextafter((float)((double)v - (double)center[k]), INFINITY); };
+    for (size_t j = 0; j < nodes.size(); j++) {
+        const hrt::SphereBvhNode& n = nodes[j];
+        float4* o = &out[4 * j];
+        o[0] = float4{rel_lo(n.lmin[0], 0), rel_lo(n.lmin[1], 1), rel_lo(n.lmin[2], 2), __builtin_bit_cast(float, n.left)};
+        o[1] = float4{rel_hi(n.lmax[0], 0), rel_hi(n.lmax[1], 1), rel_hi(n.lmax[2], 2), 0.0f};
+        o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
+        o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
+    }
+    return out;
+}
+
+int upload_tri_tree(rt_renderer* r) {
+    if (!r->tri_tree_dirty) return RT_OK;
+    r->tri_tree = hrt::build_tri_bvh(r->tri_aee);
+    const std::vector<float4> packed = pack_bvh_nodes(r->tri_tree.nodes, r->tri_tree.root_center);
+    int rc = ensure(r->tb_nodes, packed.size());
+    if (!rc) rc = ensure(r->tb_order, std::max<size_t>(r->tri_tree.order.size(), 1));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(r->tb_nodes.ptr, packed.data(), packed.size() * sizeof(float4), hipMemcpyHostToDevice,
+                           r->stream));
+    if (!r->tri_tree.order.empty())
+        HIP_TRY(hipMemcpyAsync(r->tb_order.ptr, r->tri_tree.order.data(), r->tri_tree.order.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    r->tri_tree_dirty = false;
     return RT_OK;
 }
 
@@ -177,17 +218,7 @@ int upload_spheres(rt_renderer* r) {
     }
     r->bvh_host = hrt::build_sphere_bvh(cr);
     const hrt::SphereBvh& B = r->bvh_host;
-    std::vector<float4> bnodes(4 * std::max<size_t>(B.nodes.size(), 1));
-    auto rel_lo = [&](float v, int k) { return std::nextafter((float)((double)v - (double)B.root_center[k]), -INFINITY); };
-    auto rel_hi = [&](float v, int k) { return std::nextafter((float)((double)v - (double)B.root_center[k]), INFINITY); };
-    for (size_t j = 0; j < B.nodes.size(); j++) {
-        const hrt::SphereBvhNode& n = B.nodes[j];
-        float4* o = &bnodes[4 * j];
-        o[0] = float4{rel_lo(n.lmin[0], 0), rel_lo(n.lmin[1], 1), rel_lo(n.lmin[2], 2), __builtin_bit_cast(float, n.left)};
-        o[1] = float4{rel_hi(n.lmax[0], 0), rel_hi(n.lmax[1], 1), rel_hi(n.lmax[2], 2), 0.0f};
-        o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
-        o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
-    }
+    const std::vector<float4> bnodes = pack_bvh_nodes(B.nodes, B.root_center);
     const size_t nleaf = B.slot.size();
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
@@ -289,6 +320,16 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.sph_aux = r->sph_aux.ptr;
     P.nodes = r->nodes.ptr;
     P.tris = r->tris.ptr;
+    P.tri_bvh = (r->mode != RT_MODE_SPHERE && r->params.tri_bvh) ? 1u : 0u;
+    if (P.tri_bvh) {
+        rc = upload_tri_tree(r);
+        if (rc) return rc;
+        P.tb_nodes = r->tb_nodes.ptr;
+        P.tb_order = r->tb_order.ptr;
+        P.tb_root = r->tri_tree.root_word;
+        for (int k = 0; k < 3; k++) P.tb_rc[k] = r->tri_tree.root_center[k];
+        P.tb_rr = r->tri_tree.root_radius;
+    }
     P.mats = r->mats.ptr;
     P.counter = r->counter.ptr;
 #ifdef HRT_STAMPS
@@ -537,6 +578,13 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
         d.material = t.material;
         td[j] = d;
     }
+    r->tri_aee.resize(9 * (size_t)m);
+    for (uint32_t j = 0; j < m; j++) {
+        const float v[9] = {td[j].a.x, td[j].a.y, td[j].a.z, td[j].e1.x, td[j].e1.y, td[j].e1.z,
+                            td[j].e2.x, td[j].e2.y, td[j].e2.z};
+        std::copy(v, v + 9, &r->tri_aee[9 * (size_t)j]);
+    }
+    r->tri_tree_dirty = true;
     const hrt::Material* M = (const hrt::Material*)mats32;
     std::vector<hrt_dev::MatDev> md(n_mats);
     for (uint32_t k = 0; k < n_mats; k++)

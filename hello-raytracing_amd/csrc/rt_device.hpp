@@ -90,6 +90,11 @@ struct KParams {
     uint32_t bvh_nleaf, pad_l;    // spheres in the BVH (bvh_sph / bvh_slot entries)
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
+    // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp): 4 float4 per node like bvh_nodes
+    const float4* tb_nodes;
+    const uint32_t* tb_order;     // triangle index of each leaf entry
+    uint32_t tb_root, tri_bvh;    // root child word; 1 = walk the SAH tree instead of the reference heap
+    float tb_rc[3], tb_rr;        // root box centre (nodes are relative to it) and radius bound
     const float4* nodes;          // 2 float4 per node: min, max
     const TriDev* tris;
     const MatDev* mats;

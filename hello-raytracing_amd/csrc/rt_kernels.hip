@@ -342,23 +342,25 @@ __device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3&
     return tmin <= tmax && tmax >= 0.0f;
 }
 
-// intersect_triangle, Moller-Trumbore (shader_tris.wgsl:161-202). Updates h when t in [1e-4, h.t).
-__device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_t j, Hit& h) {
-    const TriDev tr = P.tris[j];
+// intersect_triangle, Moller-Trumbore (shader_tris.wgsl:161-202): the candidate t, or -1 when the
+// determinant, u or v test rejects (the t >= 1e-4 and t < best tests are the caller's).
+__device__ __forceinline__ float tri_t(const Ray& r, const TriDev& tr) {
     const f3 e1 = mk(tr.e1.x, tr.e1.y, tr.e1.z);
     const f3 e2 = mk(tr.e2.x, tr.e2.y, tr.e2.z);
     const f3 hh = cross(r.d, e2);
     const float det = dot(e1, hh);
-    if (__builtin_fabsf(det) < 1e-4f) return;
+    if (__builtin_fabsf(det) < 1e-4f) return -1.0f;
     const float inv_det = 1.0f / det;
     const f3 s = r.o - mk(tr.a.x, tr.a.y, tr.a.z);
     const float u = inv_det * dot(s, hh);
-    if (u < 0.0f || u > 1.0f) return;
+    if (u < 0.0f || u > 1.0f) return -1.0f;
     const f3 q = cross(s, e1);
     const float v = inv_det * dot(r.d, q);
-    if (v < 0.0f || u + v > 1.0f) return;
-    const float t = inv_det * dot(e2, q);
-    if (t < 1e-4f || t >= h.t) return;
+    if (v < 0.0f || u + v > 1.0f) return -1.0f;
+    return inv_det * dot(e2, q);
+}
+
+__device__ __forceinline__ void tri_record(const KParams& P, const Ray& r, const TriDev& tr, float t, Hit& h) {
     const MatDev m = P.mats[tr.material];
     h.p = point_on_ray(r.o, r.d, t);
     h.n = mk(tr.nx, tr.ny, tr.nz);
@@ -366,6 +368,16 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
     h.ar = m.ar; h.ag = m.ag; h.ab = m.ab; h.param = m.param;
     h.id = m.id;
     h.front = dot(h.n, r.d) > 0.0f;
+}
+
+// The reference's per-leaf update: accept t in [1e-4, best). The walks only track (best, bj); the hit
+// record is built once for the winner (closest_hit), which keeps fewer registers live during the walk.
+__device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_t j, float& best, int& bj) {
+    const float t = tri_t(r, P.tris[j]);
+    if (t >= 1e-4f && t < best) {
+        best = t;
+        bj = (int)j;
+    }
 }
 
 // intersect_all_node (shader_tris.wgsl:268-301): stackless DFS over the implicit heap, 600-step cap.
@@ -376,7 +388,8 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
 // node tests, and triangle tests run with most lanes active instead of one divergent branch per step.
 constexpr uint32_t TRI_BATCH = 16;  // measured on C4: 4 -> 5.89, 8 -> 6.28, 16 -> 6.38 Grays/s
 
-__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h, Tally& tally, uint32_t* cand) {
+__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
+                                         uint32_t* cand) {
     const f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const uint32_t n = P.n, m = P.m;
     uint32_t i = 1, nc = 0, step = 0;
@@ -409,19 +422,95 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, Hit& h,
             }
             if (++step == 600u) walking = false;  // the reference's step cap
         }
-        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], h);  // in the order reached
+        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
         nc = 0;
         if (__ballot(walking) == 0ull) break;
     }
 }
 
-template <int MODE, int SCAN>
+// Opt-in triangle walk (rt_params.tri_bvh = 1; host/tri_bvh.hpp): an ordered, culling stack walk of a
+// binned-SAH BVH2 with the same Moller-Trumbore arithmetic, keeping the (t, triangle index)
+// lexicographic minimum — the winner of the reference's ordered walk, which reaches leaves in increasing
+// index and keeps the first of equal t (a sphere hit of the mixed program keeps ties, as there). Boxes
+// are padded by 2^-12 of the distance scale of the query. Not parity-exact by contract:
+// the reference's 600-step cap and unpadded slab tests can drop a triangle this walk finds. A stack
+// overflow falls back to the reference walk.
+constexpr int TRI_STACK = 24;
+
+__device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
+                                         uint32_t* stack) {
+    const f3 op = mk(r.o.x - P.tb_rc[0], r.o.y - P.tb_rc[1], r.o.z - P.tb_rc[2]);
+    const float D = __builtin_amdgcn_sqrtf(dot(op, op)) * 1.001f + P.tb_rr;
+    const float pad = D * 0x1p-12f;
+    Slab S;
+    S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+#if HRT_SLAB_FMA
+    S.lo = S.lo * S.inv;
+    S.hi = S.hi * S.inv;
+#endif
+    const float4* __restrict__ nodes = P.tb_nodes;
+    uint32_t node = P.tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
+    int sp = 0;
+    bool overflow = false;
+    while (true) {
+        if (!(node & BVH_LEAF_BIT)) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            float tl, tr;
+            const bool hl = padded_box_hit(n0, n1, S, best, tl);
+            const bool hr = padded_box_hit(n2, n3, S, best, tr);
+            tally.nodes += 2;
+            const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
+            if (hl && hr) {
+                const bool lfirst = tl <= tr;
+                if (sp < TRI_STACK) {
+                    stack[sp * 256] = lfirst ? right : left;
+                    sp++;
+                } else {
+                    overflow = true;
+                }
+                node = lfirst ? left : right;
+                continue;
+            }
+            if (hl) { node = left; continue; }
+            if (hr) { node = right; continue; }
+        } else {
+            const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint32_t j = P.tb_order[first + k];
+                const float t = tri_t(r, P.tris[j]);
+                tally.tris++;
+                if (t >= 1e-4f && (t < best || (t == best && bj >= 0 && (int)j < bj))) {
+                    best = t;
+                    bj = (int)j;
+                }
+            }
+        }
+        if (sp == 0) break;
+        node = stack[(--sp) * 256];
+    }
+    if (overflow) {  // a dropped subtree: finish with the lexicographic minimum over every triangle
+        for (uint32_t j = 0; j < P.m; j++) {
+            const float t = tri_t(r, P.tris[j]);
+            if (t >= 1e-4f && (t < best || (t == best && bj >= 0 && (int)j < bj))) {
+                best = t;
+                bj = (int)j;
+            }
+        }
+        tally.tris += P.m;
+    }
+}
+
+template <int MODE, int SCAN, bool TSAH = false>
 __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally,
-                                            uint32_t* tri_cand) {
-    h.t = FLT_MAX_REF;
+                                            uint32_t* tri_cand, uint32_t* tri_stack) {
+    float best = FLT_MAX_REF;
+    int bi = -1, bj = -1;  // winning sphere slot / triangle index
     if (MODE != MODE_TRIS) {
-        float best = FLT_MAX_REF;
-        int bi;
         if constexpr (SCAN == SCAN_BVH) {
             bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_DEFER) {
@@ -431,11 +520,23 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
             bi = scan_spheres(P, r, best);
             tally.spheres += P.nslots;
         }
-        if (bi >= 0) sphere_record(P, r, bi, best, h);
     }
-    if (MODE != MODE_SPHERE) walk_bvh(P, r, h, tally, tri_cand);
-    // abs(hit.t - FLT_MAX) < EPSILON (shader_sphere.wgsl:235): t is FLT_MAX_REF exactly or >= 2^103 away.
-    return h.t != FLT_MAX_REF;
+    if (MODE != MODE_SPHERE) {  // triangles after spheres, `t >= best` rejected: ties keep the sphere
+        if constexpr (TSAH) walk_sah(P, r, best, bj, tally, tri_stack);
+        else walk_bvh(P, r, best, bj, tally, tri_cand);
+    }
+    // every accepted t is < FLT_MAX_REF, so `abs(hit.t - FLT_MAX) < EPSILON` (shader_sphere.wgsl:235) is
+    // "nothing accepted"
+    if (bj >= 0) {
+        tri_record(P, r, P.tris[bj], best, h);
+        return true;
+    }
+    if (bi >= 0) {
+        sphere_record(P, r, bi, best, h);
+        return true;
+    }
+    h.t = FLT_MAX_REF;
+    return false;
 }
 
 // random_on_hemisphere (shader_sphere.wgsl:107-117): normalised vector in the +++ octant, flipped to n's side.
@@ -527,30 +628,34 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 // Tiles schedule (rt_params.schedule = RT_SCHEDULE_TILES): one launch = P.nframes frames over this
 // renderer's rows; a lane owns one pixel for all of them and accumulates in registers.
 // Grid: (ceil(W/16), ceil(nrows/16)).
-template <int MODE, int SCAN>
+template <int MODE, int SCAN, bool TSAH = false>
 __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* lds_list = nullptr;
-    uint32_t* tri_cand = nullptr;  // triangle program: deferred triangle list (aliases the sphere scan's
-                                   // LDS list, which is free again once the sphere scan has returned)
+    // triangle program: the deferred triangle list of the reference walk and the stack of the opt-in SAH
+    // walk share one per-lane LDS area (never live together; a SAH stack overflow restarts with the
+    // reference walk), which also aliases the sphere scan's list once the sphere scan has returned
+    uint32_t* tri_cand = nullptr;
+    constexpr int TRI_WORDS = (int)TRI_BATCH > TRI_STACK ? (int)TRI_BATCH : TRI_STACK;
     if constexpr (SCAN == SCAN_DEFER) {
         // (the u16 sphere list cannot alias the u32 triangle list: the lane strides differ, so one wave's
         // entries would overlap another wave's)
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
         if constexpr (MODE != MODE_SPHERE) {
-            __shared__ uint32_t tri_list_d[TRI_BATCH * 256];
+            __shared__ uint32_t tri_list_d[TRI_WORDS * 256];
             tri_cand = tri_list_d + threadIdx.x;
         }
     } else if constexpr (SCAN == SCAN_BVH) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-        static_assert(BVH_STACK >= (int)TRI_BATCH, "tri list alias");
+        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
         lds_list = bvh_stack + threadIdx.x;
         tri_cand = bvh_stack + threadIdx.x;
     } else if constexpr (MODE != MODE_SPHERE) {
-        __shared__ uint32_t tri_list[TRI_BATCH * 256];
+        __shared__ uint32_t tri_list[TRI_WORDS * 256];
         tri_cand = tri_list + threadIdx.x;
     }
+    uint32_t* const tri_stack = tri_cand;
     Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
@@ -589,7 +694,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 #endif
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, tri_cand);
+            const bool hit = closest_hit<MODE, SCAN, TSAH>(P, ray, h, lds_list, tally, tri_cand, tri_stack);
             queries++;
 #ifdef HRT_STAMPS
             st_tb = hrt_stamp();
@@ -701,31 +806,35 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // 768 contiguous bytes, so colour stores fill whole cache lines); k_accumulate then folds
 // the colours into the image in frame order per pixel with the reference's mix
 // (shader_sphere.wgsl:264-271), so the image is bit-identical to k_render's and to count x rt_draw.
-template <int MODE, int SCAN>
+template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace(const KParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 6))) void k_trace(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     void* lds_list = nullptr;
-    uint32_t* tri_cand = nullptr;  // triangle program: deferred triangle list (aliases the sphere scan's
-                                   // LDS list, which is free again once the sphere scan has returned)
+    // triangle program: the deferred triangle list of the reference walk and the stack of the opt-in SAH
+    // walk share one per-lane LDS area (never live together; a SAH stack overflow restarts with the
+    // reference walk), which also aliases the sphere scan's list once the sphere scan has returned
+    uint32_t* tri_cand = nullptr;
+    constexpr int TRI_WORDS = (int)TRI_BATCH > TRI_STACK ? (int)TRI_BATCH : TRI_STACK;
     if constexpr (SCAN == SCAN_DEFER) {
         // (the u16 sphere list cannot alias the u32 triangle list: the lane strides differ, so one wave's
         // entries would overlap another wave's)
         __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
         lds_list = cand + threadIdx.x;
         if constexpr (MODE != MODE_SPHERE) {
-            __shared__ uint32_t tri_list_d[TRI_BATCH * 256];
+            __shared__ uint32_t tri_list_d[TRI_WORDS * 256];
             tri_cand = tri_list_d + threadIdx.x;
         }
     } else if constexpr (SCAN == SCAN_BVH) {
         __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-        static_assert(BVH_STACK >= (int)TRI_BATCH, "tri list alias");
+        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
         lds_list = bvh_stack + threadIdx.x;
         tri_cand = bvh_stack + threadIdx.x;
     } else if constexpr (MODE != MODE_SPHERE) {
-        __shared__ uint32_t tri_list[TRI_BATCH * 256];
+        __shared__ uint32_t tri_list[TRI_WORDS * 256];
         tri_cand = tri_list + threadIdx.x;
     }
+    uint32_t* const tri_stack = tri_cand;
     Tally tally;
     uint32_t queries = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -800,7 +909,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
-            const bool hit = closest_hit<MODE, SCAN>(P, ray, h, lds_list, tally, tri_cand);
+            const bool hit = closest_hit<MODE, SCAN, TSAH>(P, ray, h, lds_list, tally, tri_cand, tri_stack);
             queries++;
 #ifdef HRT_STAMPS
             st_ta = hrt_stamp();
@@ -908,24 +1017,29 @@ static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stre
 }
 
 // Sample queue, part 1: trace every sample of the chunk into P.samples.
-// variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (others are resolved to SCAN_BVH by the host).
+// variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host); P.tri_bvh picks the triangle walk.
+template <int MODE, bool TSAH>
+static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t stream) {
+    if constexpr (MODE == MODE_TRIS) {
+        return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream);
+    } else {
+        if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream);
+        if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream);
+        return launch_persistent(k_trace<MODE, SCAN_BVH, TSAH>, P, stream);
+    }
+}
+
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {
     if (P.njobs == 0) return hipSuccess;
-    hipError_t e;
     switch (mode) {
-    case MODE_SPHERE:
-        if (variant == SCAN_SIMPLE) e = launch_persistent(k_trace<MODE_SPHERE, SCAN_SIMPLE>, P, stream);
-        else if (variant == SCAN_DEFER) e = launch_persistent(k_trace<MODE_SPHERE, SCAN_DEFER>, P, stream);
-        else e = launch_persistent(k_trace<MODE_SPHERE, SCAN_BVH>, P, stream);
-        break;
-    case MODE_TRIS: e = launch_persistent(k_trace<MODE_TRIS, SCAN_SIMPLE>, P, stream); break;
+    case MODE_SPHERE: return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
+    case MODE_TRIS:
+        return P.tri_bvh ? launch_trace_mode<MODE_TRIS, true>(variant, P, stream)
+                         : launch_trace_mode<MODE_TRIS, false>(variant, P, stream);
     default:
-        if (variant == SCAN_SIMPLE) e = launch_persistent(k_trace<MODE_MIXED, SCAN_SIMPLE>, P, stream);
-        else if (variant == SCAN_DEFER) e = launch_persistent(k_trace<MODE_MIXED, SCAN_DEFER>, P, stream);
-        else e = launch_persistent(k_trace<MODE_MIXED, SCAN_BVH>, P, stream);
-        break;
+        return P.tri_bvh ? launch_trace_mode<MODE_MIXED, true>(variant, P, stream)
+                         : launch_trace_mode<MODE_MIXED, false>(variant, P, stream);
     }
-    return e;
 }
 
 // Sample queue, part 2: fold the chunk's colours into the image in frame order.
@@ -938,21 +1052,30 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 
 // Host-side launcher of the tiles schedule (called from renderer.cpp; no HIP types in the C-ABI).
 // variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host).
+template <int MODE, bool TSAH>
+static void launch_render_mode(int variant, const KParams& P, dim3 grid, dim3 block, hipStream_t stream) {
+    if constexpr (MODE == MODE_TRIS) {
+        hipLaunchKernelGGL((k_render<MODE, SCAN_SIMPLE, TSAH>), grid, block, 0, stream, P);
+    } else {
+        if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE, SCAN_SIMPLE, TSAH>), grid, block, 0, stream, P);
+        else if (variant == SCAN_DEFER) hipLaunchKernelGGL((k_render<MODE, SCAN_DEFER, TSAH>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((k_render<MODE, SCAN_BVH, TSAH>), grid, block, 0, stream, P);
+    }
+}
+
 hipError_t hrt_launch_render(int mode, int variant, const KParams& P, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((P.W + 15u) / 16u, (P.nrows + 15u) / 16u);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     switch (mode) {
-    case MODE_SPHERE:
-        if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_SIMPLE>), grid, block, 0, stream, P);
-        else if (variant == SCAN_DEFER) hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_DEFER>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((k_render<MODE_SPHERE, SCAN_BVH>), grid, block, 0, stream, P);
+    case MODE_SPHERE: launch_render_mode<MODE_SPHERE, false>(variant, P, grid, block, stream); break;
+    case MODE_TRIS:
+        if (P.tri_bvh) launch_render_mode<MODE_TRIS, true>(variant, P, grid, block, stream);
+        else launch_render_mode<MODE_TRIS, false>(variant, P, grid, block, stream);
         break;
-    case MODE_TRIS: hipLaunchKernelGGL((k_render<MODE_TRIS, SCAN_SIMPLE>), grid, block, 0, stream, P); break;
     default:
-        if (variant == SCAN_SIMPLE) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_SIMPLE>), grid, block, 0, stream, P);
-        else if (variant == SCAN_DEFER) hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_DEFER>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((k_render<MODE_MIXED, SCAN_BVH>), grid, block, 0, stream, P);
+        if (P.tri_bvh) launch_render_mode<MODE_MIXED, true>(variant, P, grid, block, stream);
+        else launch_render_mode<MODE_MIXED, false>(variant, P, grid, block, stream);
         break;
     }
     return hipGetLastError();

@@ -40,6 +40,7 @@ class RtParams(C.Structure):
         ("schedule", C.c_uint32),
         ("queue_budget_mb", C.c_uint32),
         ("job_frames", C.c_uint32),
+        ("tri_bvh", C.c_uint32),
     ]
 
 

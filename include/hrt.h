@@ -70,6 +70,10 @@ typedef struct rt_params {
                                   order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 8        */
+    uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
+                                  parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
+                                  same closest hit except where the reference's 600-step cap or
+                                  unpadded slab tests drop a triangle (non-parity)  */
 } rt_params;
 
 #define RT_SCHEDULE_AUTO 0u

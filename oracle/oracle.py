@@ -20,7 +20,8 @@ MODE_SPHERE, MODE_TRIS, MODE_MIXED = 0, 1, 2
 
 class OParams(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("width", "height", "mode", "bounces", "ema_cap", "frame0", "time0",
-                                          "dtime", "frames", "x0", "nx", "row0", "row_step", "nrows")]
+                                          "dtime", "frames", "x0", "nx", "row0", "row_step", "nrows",
+                                          "step_cap")]
 
 
 _lib = None
@@ -51,12 +52,14 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
            dtime: int = 10, frame0: int = 0, bounces: int | None = None, ema_cap: int = 1000,
            spheres: np.ndarray | None = None, min_sphere_slots: int | None = None, bvh=None,
            rows=None, x0: int = 0, nx: int | None = None, image: np.ndarray | None = None,
-           threads: int = 0):
+           threads: int = 0, step_cap: int = 600):
     """Render `frames` frames (time0 + f*dtime, frame_count frame0 + f) of a scene.
 
     spheres: SPHERE_DTYPE array (zero slots appended up to min_sphere_slots, default 100 in sphere mode
     like the reference's 100-slot buffer); bvh: (sizes, nodes, triangles, materials) from Tree.view().
     rows: (row0, row_step, nrows) subset of rows (global coordinates), default all rows.
+    step_cap: the reference walk's 600-step cap (shader_tris.wgsl:274); 0 = uncapped (only to check the
+    opt-in SAH triangle walk, which has no cap).
     Returns (image[nrows, nx, 3] float32, queries).
     """
     if bounces is None:
@@ -65,7 +68,8 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
         min_sphere_slots = 100 if mode == MODE_SPHERE else 0
     row0, row_step, nrows = rows if rows is not None else (0, 1, height)
     nx = width - x0 if nx is None else nx
-    p = OParams(width, height, mode, bounces, ema_cap, frame0, time0, dtime, frames, x0, nx, row0, row_step, nrows)
+    p = OParams(width, height, mode, bounces, ema_cap, frame0, time0, dtime, frames, x0, nx, row0, row_step, nrows,
+                step_cap)
     sph_ptr, nslots, keep = None, 0, []
     if mode != MODE_TRIS:
         sp = spheres if spheres is not None else np.zeros(0, dtype=np.uint8)
@@ -95,10 +99,10 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
     cam = np.ascontiguousarray(camera).tobytes()
     if threads <= 0:  # explicit: importing torch can leave the OpenMP default at one thread
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    counts = (C.c_uint64 * 3)()
+    counts = (C.c_uint64 * 4)()
     q = lib().oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
                             image.ctypes.data, threads, counts)
-    last_counts.update(rays=counts[0], node_tests=counts[1], tri_tests=counts[2])
+    last_counts.update(rays=counts[0], node_tests=counts[1], tri_tests=counts[2], capped_walks=counts[3])
     return image, int(q)
 
 

@@ -56,6 +56,8 @@ typedef struct {
     uint32_t frames;          /* frames drawn by this call                                       */
     uint32_t x0, nx;          /* column window                                                   */
     uint32_t row0, row_step, nrows; /* rows row0 + k*row_step, k < nrows                         */
+    uint32_t step_cap;        /* intersect_all_node step cap: 600 in the reference (shader_tris.wgsl:274);
+                                 0 = uncapped, only to check the opt-in SAH walk (non-parity mode)   */
 } o_params;
 
 typedef struct { float x, y, z; } v3;
@@ -93,6 +95,7 @@ typedef struct {
     const o_sphere *spheres; uint32_t nslots;
     const o_node *nodes; const o_triangle *tris; const o_material *mats; uint32_t n, m;
     uint32_t mode, bounces; float eps;
+    uint32_t step_cap;
 } o_scene;
 
 /* random_on_hemisphere: shader_sphere.wgsl:107-117 / shader_tris.wgsl:119-128 */
@@ -200,8 +203,9 @@ static inline void tri_test(const o_scene *sc, ray_t r, uint32_t j, hit_t *h) {
 static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h, uint64_t *cnt) {
     v3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     uint32_t i = 1, n = sc->n, m = sc->m;
-    int step = 0;
-    while (step < 600) {
+    const uint32_t cap = sc->step_cap ? sc->step_cap : 0xFFFFFFFFu;
+    uint32_t step = 0;
+    while (step < cap) {
         step++;
         if (i < n) {
             cnt[1]++; /* node (slab) tests */
@@ -217,6 +221,7 @@ static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h, uint64_t *cnt) {
         if (i == 0u) break;
         i++;
     }
+    if (step == cap && i != 0u) cnt[3]++; /* walks the step cap cut short (bookkeeping, not semantics) */
 }
 
 static inline v3 reflect3(v3 v, v3 n) { return vsub(v, smul(2.0f * dot3(v, n), n)); }
@@ -304,7 +309,7 @@ static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, ui
  * layout ((k*nx) + (x-x0))*3), continuing the accumulation already in `image` exactly as
  * repeated Renderer::draw() calls do (renderer.rs:355-410, accumulation at shader_sphere.wgsl:264-271).
  * Returns the number of closest-hit queries (rays) traced; if `counts` is given it receives
- * {rays, triangle-program node tests, triangle tests}.
+ * {rays, triangle-program node tests, triangle tests, walks cut short by the 600-step cap}.
  */
 uint64_t oracle_render(const o_params *p, const void *camera80, const void *spheres48, uint32_t nslots,
                        const uint32_t *sizes, const void *nodes32, const void *tris64, const void *mats32,
@@ -315,16 +320,16 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
     sc.spheres = (const o_sphere *)spheres48; sc.nslots = spheres48 ? nslots : 0;
     sc.nodes = (const o_node *)nodes32; sc.tris = (const o_triangle *)tris64; sc.mats = (const o_material *)mats32;
     sc.n = sizes ? sizes[0] : 0; sc.m = sizes ? sizes[1] : 0;
-    sc.mode = p->mode; sc.bounces = p->bounces;
+    sc.mode = p->mode; sc.bounces = p->bounces; sc.step_cap = p->step_cap;
     sc.eps = p->mode == MODE_SPHERE ? 1e-6f : 1e-4f;
-    uint64_t total = 0, tnodes = 0, ttris = 0;
+    uint64_t total = 0, tnodes = 0, ttris = 0, tcapped = 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, tnodes, ttris)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, tnodes, ttris, tcapped)
 #endif
     for (int64_t k = 0; k < (int64_t)p->nrows; k++) {
         uint32_t y = p->row0 + (uint32_t)k * p->row_step;
-        uint64_t q[3] = {0, 0, 0};
+        uint64_t q[4] = {0, 0, 0, 0};
         for (uint32_t x = p->x0; x < p->x0 + p->nx; x++) {
             float *px = image + ((size_t)k * p->nx + (x - p->x0)) * 3;
             float r = px[0], g = px[1], b = px[2];
@@ -342,11 +347,13 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
         total += q[0];
         tnodes += q[1];
         ttris += q[2];
+        tcapped += q[3];
     }
     if (counts) {
         counts[0] = total;
         counts[1] = tnodes;
         counts[2] = ttris;
+        counts[3] = tcapped;
     }
     return total;
 }
