@@ -529,6 +529,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->variant != 0 && p->variant != 1 && p->variant != 3 && p->variant != 4)
         return fail(RT_ERR_ARG, "rt_set_params: unknown variant (0 auto, 1 simple, 3 deferred, 4 culling BVH)");
     if (p->schedule > RT_SCHEDULE_QUEUE) return fail(RT_ERR_ARG, "rt_set_params: unknown schedule");
+    if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;

@@ -414,6 +414,31 @@ def test_large_frame_count_ema_regime():
     assert_parity(r.read_image(), ref, "frames 998..1002")
 
 
+def test_rendering_performance():
+    """tests/rendering_tests.rs:527-578: 20 spheres on a ring + ground, 512x512, must finish in < 5 s.
+    The reference times command submission only; here the draws are synchronised, and 100 frames (the
+    comment's count, TEST_FRAMES is 1 in the file) through the per-frame protocol."""
+    import math
+    import time
+    scene = hrt.SceneSphere.new(512, 512)
+    scene.objects.clear()
+    for i in range(20):
+        angle = np.float32(i) * np.float32(math.pi) * np.float32(2.0) / np.float32(20.0)
+        x, z = float(np.cos(angle) * np.float32(3.0)), float(np.float32(-5.0) + np.sin(angle) * np.float32(3.0))
+        scene.objects.append(hrt.Sphere.new_lambertian(hrt.Vec3(x, 0.0, z), 0.4,
+                                                       hrt.Vec3(i / 20.0, 0.5, 1.0 - i / 20.0)))
+    scene.objects.append(hrt.Sphere.new_lambertian(hrt.Vec3(0.0, -100.4, -5.0), 100.0, hrt.Vec3(0.5, 0.5, 0.5)))
+    scene.init()
+    t0 = time.perf_counter()
+    for i in range(100):
+        scene.set_time(1000 + i * 10)
+        scene.draw()
+    scene.renderer.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert elapsed < 5.0, f"Rendering took too long: {elapsed:.3f} s"
+    assert np.isfinite(scene.renderer.read_image()).all()
+
+
 def test_bad_arguments_fail_loudly():
     r = hrt.Renderer(8, 8, hrt.RT_MODE_TRIS)
     with pytest.raises(hrt.RtError):  # draw before set_camera
@@ -427,3 +452,6 @@ def test_bad_arguments_fail_loudly():
                     np.zeros(1, dtype=hrt.MATERIAL_DTYPE))
     small = np.zeros(10, dtype=np.float32)
     assert hrt.lib().rt_read_image(r._h, small.ctypes.data_as(hrt._lib._PF), small.size) == hrt._lib.RT_ERR_ARG
+    for bad in ({"variant": 2}, {"variant": 9}, {"schedule": 3}, {"tri_bvh": 2}, {"row_step": 0}):
+        with pytest.raises(hrt.RtError):  # removed variants, unknown schedule / tree, empty partition
+            r.set_params(**bad)
