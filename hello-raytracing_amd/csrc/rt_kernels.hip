@@ -623,6 +623,39 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
     return r;
 }
 
+// Per-lane LDS lists of a 256-lane workgroup (lane stride 256): the sphere scan's candidate list or
+// stack, and the triangle program's deferred-triangle list, which is also the opt-in SAH walk's stack
+// (never live together). The triangle list aliases the sphere BVH stack, free again once the sphere scan
+// has returned; the u16 candidate list of the deferred scan cannot be aliased (its lane stride differs,
+// so one wave's entries would overlap another wave's).
+struct LaneLists {
+    void* sphere;
+    uint32_t* tri;
+};
+
+template <int MODE, int SCAN>
+__device__ __forceinline__ LaneLists lane_lists() {
+    LaneLists L{nullptr, nullptr};
+    constexpr int TRI_WORDS = (int)TRI_BATCH > TRI_STACK ? (int)TRI_BATCH : TRI_STACK;
+    if constexpr (SCAN == SCAN_DEFER) {
+        __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
+        L.sphere = cand + threadIdx.x;
+        if constexpr (MODE != MODE_SPHERE) {
+            __shared__ uint32_t tri_list_d[TRI_WORDS * 256];
+            L.tri = tri_list_d + threadIdx.x;
+        }
+    } else if constexpr (SCAN == SCAN_BVH) {
+        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
+        L.sphere = bvh_stack + threadIdx.x;
+        L.tri = bvh_stack + threadIdx.x;
+    } else if constexpr (MODE != MODE_SPHERE) {
+        __shared__ uint32_t tri_list[TRI_WORDS * 256];
+        L.tri = tri_list + threadIdx.x;
+    }
+    return L;
+}
+
 }  // namespace
 
 // Tiles schedule (rt_params.schedule = RT_SCHEDULE_TILES): one launch = P.nframes frames over this
@@ -631,31 +664,10 @@ __device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_
 template <int MODE, int SCAN, bool TSAH = false>
 __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    void* lds_list = nullptr;
-    // triangle program: the deferred triangle list of the reference walk and the stack of the opt-in SAH
-    // walk share one per-lane LDS area (never live together; a SAH stack overflow restarts with the
-    // reference walk), which also aliases the sphere scan's list once the sphere scan has returned
-    uint32_t* tri_cand = nullptr;
-    constexpr int TRI_WORDS = (int)TRI_BATCH > TRI_STACK ? (int)TRI_BATCH : TRI_STACK;
-    if constexpr (SCAN == SCAN_DEFER) {
-        // (the u16 sphere list cannot alias the u32 triangle list: the lane strides differ, so one wave's
-        // entries would overlap another wave's)
-        __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
-        lds_list = cand + threadIdx.x;
-        if constexpr (MODE != MODE_SPHERE) {
-            __shared__ uint32_t tri_list_d[TRI_WORDS * 256];
-            tri_cand = tri_list_d + threadIdx.x;
-        }
-    } else if constexpr (SCAN == SCAN_BVH) {
-        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
-        lds_list = bvh_stack + threadIdx.x;
-        tri_cand = bvh_stack + threadIdx.x;
-    } else if constexpr (MODE != MODE_SPHERE) {
-        __shared__ uint32_t tri_list[TRI_WORDS * 256];
-        tri_cand = tri_list + threadIdx.x;
-    }
-    uint32_t* const tri_stack = tri_cand;
+    const LaneLists lists = lane_lists<MODE, SCAN>();
+    void* const lds_list = lists.sphere;
+    uint32_t* const tri_cand = lists.tri;
+    uint32_t* const tri_stack = lists.tri;
     Tally tally;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
@@ -810,31 +822,10 @@ template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 6))) void k_trace(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u;
-    void* lds_list = nullptr;
-    // triangle program: the deferred triangle list of the reference walk and the stack of the opt-in SAH
-    // walk share one per-lane LDS area (never live together; a SAH stack overflow restarts with the
-    // reference walk), which also aliases the sphere scan's list once the sphere scan has returned
-    uint32_t* tri_cand = nullptr;
-    constexpr int TRI_WORDS = (int)TRI_BATCH > TRI_STACK ? (int)TRI_BATCH : TRI_STACK;
-    if constexpr (SCAN == SCAN_DEFER) {
-        // (the u16 sphere list cannot alias the u32 triangle list: the lane strides differ, so one wave's
-        // entries would overlap another wave's)
-        __shared__ uint16_t cand[(CAND_CAP + 1) * 256];
-        lds_list = cand + threadIdx.x;
-        if constexpr (MODE != MODE_SPHERE) {
-            __shared__ uint32_t tri_list_d[TRI_WORDS * 256];
-            tri_cand = tri_list_d + threadIdx.x;
-        }
-    } else if constexpr (SCAN == SCAN_BVH) {
-        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
-        lds_list = bvh_stack + threadIdx.x;
-        tri_cand = bvh_stack + threadIdx.x;
-    } else if constexpr (MODE != MODE_SPHERE) {
-        __shared__ uint32_t tri_list[TRI_WORDS * 256];
-        tri_cand = tri_list + threadIdx.x;
-    }
-    uint32_t* const tri_stack = tri_cand;
+    const LaneLists lists = lane_lists<MODE, SCAN>();
+    void* const lds_list = lists.sphere;
+    uint32_t* const tri_cand = lists.tri;
+    uint32_t* const tri_stack = lists.tri;
     Tally tally;
     uint32_t queries = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
