@@ -841,6 +841,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
     bool have = false;
 #ifdef HRT_STAMPS
     unsigned long long st_trav = 0, st_shade = 0, st_gen = 0, st_ta, st_tb;
+    unsigned long long st_pq = 0, st_pbox = 0, st_ptrav = 0;
     const unsigned long long st_start = hrt_stamp();
     const unsigned long long rt_start = hrt_realtime();
 #endif
@@ -900,11 +901,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
         bool done = true;
         if (bounce < P.bounces) {
             Hit h;
+#ifdef HRT_STAMPS
+            const uint32_t boxes0 = tally.boxes;
+#endif
             const bool hit = closest_hit<MODE, SCAN, TSAH>(P, ray, h, lds_list, tally, tri_cand, tri_stack);
             queries++;
 #ifdef HRT_STAMPS
             st_ta = hrt_stamp();
             st_trav += st_ta - st_tb;
+            if (bounce == 0) {  // primary queries: count, box tests, lane-cycles
+                st_pq++;
+                st_pbox += tally.boxes - boxes0;
+                st_ptrav += st_ta - st_tb;
+            }
             st_tb = st_ta;
 #endif
             if (hit) {
@@ -933,9 +942,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)
-        unsigned long long v[5] = {st_trav, st_shade, st_gen, hrt_stamp() - st_start, queries};
+        unsigned long long v[8] = {st_trav, st_shade, st_gen, hrt_stamp() - st_start, queries,
+                                   st_pq, st_pbox, st_ptrav};
 #pragma unroll
-        for (int c = 0; c < 5; c++) {
+        for (int c = 0; c < 8; c++) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
         }
@@ -945,6 +955,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
             atomicAdd(P.counter + 12, r1 - rt_start);
             atomicAdd(P.counter + 13, 1ull);
             atomicAdd(P.counter + 14, t1 - st_start);
+            atomicAdd(P.counter + 5, v[5]);  // primary queries, their box tests and lane-cycles
+            atomicAdd(P.counter + 6, v[6]);
+            atomicAdd(P.counter + 7, v[7]);
         }
     }
 #endif

@@ -79,6 +79,10 @@ def main() -> None:
             "share_query": trav / life, "share_shade": shade / life, "share_gen": gen / life,
             "share_idle": 1.0 - (trav + shade + gen) / life,
             "lane_cycles_per_query": trav / max(1, st.queries),
+            "primary_queries": int(q[5]), "box_tests_per_primary": q[6] / max(1, q[5]),
+            "box_tests_per_secondary": (st.box_tests - q[6]) / max(1, st.queries - q[5]),
+            "lane_cycles_per_primary": q[7] / max(1, q[5]),
+            "lane_cycles_per_secondary": (trav - q[7]) / max(1, st.queries - q[5]),
             # s_memtime ticks per s_memrealtime tick (x 100 MHz = memtime clock), and the mean number of
             # resident waves per SIMD over the draw (wave-lifetime sum / (draw time x 1024 SIMDs))
             "memtime_mhz": 100.0 * q[14] / max(1, q[12]),

@@ -414,6 +414,37 @@ def test_large_frame_count_ema_regime():
     assert_parity(r.read_image(), ref, "frames 998..1002")
 
 
+def test_resize_and_scene_truncation():
+    """Renderer::resize (renderer.rs:271-313) zeroes the image and the frame counter: rendering after a
+    resize equals a fresh renderer of the new size, bit for bit. SceneSphere::write_scene_data
+    (scene_sphere.rs:24-31) keeps only the first 100 objects of a longer list."""
+    sd = scenes.golden_scene("metal_materials", 48, 40)
+    r = scenes.make_renderer(sd)
+    r.draw_frames(3, 1000, 10)
+    r.resize(40, 30)
+    assert r.frame_count == 0 and not r.read_image().any()
+    r.draw_frames(4, 1000, 10)
+    sd2 = scenes.golden_scene("metal_materials", 40, 30)
+    fresh = scenes.make_renderer(sd2)
+    fresh.draw_frames(4, 1000, 10)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), fresh.read_image().view(np.uint32))
+
+    scene = hrt.SceneSphere.new(32, 24)
+    scene.objects.clear()
+    for i in range(120):  # the last 20 would hide everything if they were drawn
+        scene.objects.append(hrt.Sphere.new_lambertian(hrt.Vec3(float(i % 10) - 4.5, float(i // 10) * 0.2, -6.0),
+                                                       0.3, hrt.Vec3(0.2, 0.6, 0.4)))
+    scene.objects[100:] = [hrt.Sphere.new_lambertian(hrt.Vec3(0.0, 0.0, 2.0), 1.5, hrt.Vec3(1, 0, 0))] * 20
+    scene.init()
+    for i in range(3):
+        scene.set_time(1000 + 10 * i)
+        scene.draw()
+    sdt = scenes.SceneDef("trunc", hrt.RT_MODE_SPHERE, 32, 24, scene.camera, hrt.spheres_array(scene.objects[:100]),
+                          frames=3)
+    ref, _ = scenes.oracle_render(sdt)
+    assert_parity(scene.renderer.read_image(), ref, "100-sphere truncation")
+
+
 def test_rendering_performance():
     """tests/rendering_tests.rs:527-578: 20 spheres on a ring + ground, 512x512, must finish in < 5 s.
     The reference times command submission only; here the draws are synchronised, and 100 frames (the
