@@ -645,8 +645,8 @@ __device__ __forceinline__ LaneLists lane_lists() {
             L.tri = tri_list_d + threadIdx.x;
         }
     } else if constexpr (SCAN == SCAN_BVH) {
-        __shared__ uint32_t bvh_stack[BVH_STACK * 256];
-        static_assert(BVH_STACK >= TRI_WORDS, "tri list alias");
+        constexpr int WORDS = MODE == MODE_SPHERE || BVH_STACK >= TRI_WORDS ? BVH_STACK : TRI_WORDS;
+        __shared__ uint32_t bvh_stack[WORDS * 256];
         L.sphere = bvh_stack + threadIdx.x;
         L.tri = bvh_stack + threadIdx.x;
     } else if constexpr (MODE != MODE_SPHERE) {
