@@ -37,6 +37,33 @@ NODE_TEST_FLOP = 27  # implicit-heap slab test (3 rcp-mul pairs, 
 TRI_TEST_FLOP = 51  # Moller-Trumbore
 
 
+def golden_check():
+    """The reference's golden images (tests/golden, rendering_tests.rs:134-509) rendered on the GPU with their
+    protocol (512x512, 100 frames, time 1000 + 10 i), compared in render_ppm's u8 space: per-channel max and
+    mean |delta| as a fraction of 255, exact-u8 fraction, and compare_ppm_images' 2 % rule. Glass scenes differ
+    from the golden GPU by construction; HIP vs the CPU oracle is bit-exact (tests/)."""
+    import numpy as np
+
+    import hrt
+    import scenes
+
+    per = {}
+    for name in scenes.GOLDEN_NAMES:
+        sd = scenes.golden_scene(name)
+        r = scenes.make_renderer(sd)
+        r.draw_frames(scenes.GOLDEN_FRAMES, 1000, 10)
+        img = r.read_image()
+        golden = scenes.load_golden_u8(name)
+        d = np.abs(scenes.to_u8(img).astype(np.int32) - golden.astype(np.int32))
+        pct = hrt.compare_ppm_images(hrt.render_ppm(r), scenes.ppm_text_from_u8(golden), 2.0)
+        per[name] = {"max_abs_delta": round(float(d.max()) / 255.0, 5), "mean_abs_delta": round(float(d.mean()) / 255.0, 6),
+                     "exact_u8": round(float(np.mean(d == 0)), 5), "harness_pct": round(float(pct), 4)}
+    non_glass = [v["max_abs_delta"] for k, v in per.items() if k not in scenes.GLASS_GOLDENS]
+    return {"scenes": len(per), "harness_pass": sum(v["harness_pct"] <= 2.0 for v in per.values()),
+            "max_abs_delta_non_glass": max(non_glass),
+            "max_abs_delta_all": max(v["max_abs_delta"] for v in per.values()), "per_scene": per}
+
+
 def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -76,6 +103,9 @@ def main() -> int:
     ap.add_argument("--frames-per-launch", type=int, default=1024, help="tiles schedule: frames per launch")
     ap.add_argument("--schedule", type=int, default=0, help="0 auto (queue), 1 tiles, 2 sample queue")
     ap.add_argument("--job-frames", type=int, default=8, help="sample queue: frames per 8x8-tile job")
+    ap.add_argument("--suspend-below", type=int, default=None,
+                    help="sample queue, sphere BVH: suspend a wave's walks below this many walking lanes "
+                         "(default: the library's)")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -84,6 +114,7 @@ def main() -> int:
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--verify", action="store_true", help="rank 0 re-renders the image alone and compares")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=64)
     args = ap.parse_args()
@@ -122,8 +153,9 @@ def main() -> int:
         sd.frames = args.frames or sd.frames
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
+    extra = {} if args.suspend_below is None else {"suspend_below": args.suspend_below}
     r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
-                 schedule=args.schedule, job_frames=args.job_frames, tri_bvh=args.tri_bvh)
+                 schedule=args.schedule, job_frames=args.job_frames, tri_bvh=args.tri_bvh, **extra)
     local_rows = r.local_rows
     max_rows = (sd.height + world - 1) // world
     part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
@@ -280,6 +312,10 @@ def main() -> int:
         if not args.no_cpu_baseline and world == 1:
             log("cpu baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline(sd, min(16, os.cpu_count() or 1), args.cpu_rows, args.cpu_frames)
+        if not args.no_golden:
+            out["golden"] = golden_check()
+            log(f"golden: {out['golden']['harness_pass']}/{out['golden']['scenes']} pass the reference harness, "
+                f"max |delta| {out['golden']['max_abs_delta_non_glass']} (non-glass)")
         if args.verify:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)

@@ -106,6 +106,8 @@ struct KParams {
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
     uint32_t job_frames, nchunks; // frames per job (a job = one tile x job_frames frames), chunks per tile
+    uint32_t suspend_below;       // k_trace_split: suspend the walks once fewer lanes than this still walk
+    uint32_t pad_q;
 };
 
 struct f3 {

@@ -226,30 +226,52 @@ __device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx,
 // visited sphere is tested with the reference arithmetic, and the winner is the (t, slot) minimum.
 // Rays the bound does not cover (non-finite origin, 2a outside [2^-100, 2^100]) or a stack overflow fall
 // back to the full exact scan. `stack` is this lane's slot of the workgroup's LDS stack (stride 256).
-__device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
-                                                Tally& tally) {
+//
+// The query is split in three so a traversal can be suspended and resumed (k_trace_split): bvh_begin
+// (large list, slab constants), bvh_run (the walk; with SUSPEND it returns early once fewer than
+// `below` lanes of the wave are still walking, leaving the state in BvhQuery and the LDS stack) and
+// bvh_end (winner slot, or the exact full scan for the fallback cases).
+struct BvhQuery {
+    Slab S;
+    float a4, a2, bt;
+    int bc;          // running winner as a code: BVH-order position (< nleaf) or nleaf + large-list index
+    uint32_t node;   // next child word to visit
+    int sp;
+    uint32_t full_scan;  // uncovered ray or stack overflow: bvh_end runs the exact full scan
+};
+
+__device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
+    return (uint32_t)code < P.bvh_nleaf ? P.bvh_slot[code] : P.large_slots[code - (int)P.bvh_nleaf];
+}
+
+// Returns true when the walk has to run (false: bvh_end does the full scan).
+__device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
+    Q.a4 = 4.0f * a;
+    Q.a2 = 2.0f * a;
+    Q.sp = 0;
     const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
-    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
-        tally.spheres += P.nslots;
-        return scan_spheres(P, r, best);
+    if (!(Q.a2 > 0x1p-100f && Q.a2 < 0x1p100f) || !finite_o) {
+        Q.full_scan = 1u;
+#ifdef HRT_DEBUG_SPLIT
+        atomicAdd(P.counter + 5, 1ull);
+#endif
+        return false;
     }
-    // The running winner is kept as a code: BVH-order position (< nleaf) or nleaf + large-list index, so
-    // a leaf test needs no slot load; slots are fetched only to break an exact t tie and at the end.
+    Q.full_scan = 0u;
+    // The running winner is kept as a code, so a leaf test needs no slot load; slots are fetched only
+    // to break an exact t tie and at the end.
     const uint32_t nleaf = P.bvh_nleaf;
-    auto slot_of = [&](int code) -> int {
-        return (uint32_t)code < nleaf ? P.bvh_slot[code] : P.large_slots[code - (int)nleaf];
-    };
     float bt = best;
     int bc = -1;
     for (uint32_t k = 0; k < P.nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
-        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
-        if (beats(t, i, bt, bc >= 0 ? slot_of(bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
+        const float t = exact_t_geo(P.sph_geo[i], r, Q.a4, Q.a2);
+        if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
     tally.spheres += P.nlarge;
+    Q.bt = bt;
+    Q.bc = bc;
 
     // per-query padding: delta >= the distance by which a float-accepted sphere can miss geometrically
     const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
@@ -258,19 +280,32 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     const float dn = __builtin_amdgcn_sqrtf(a);
     const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
     const float pad = 2.02f * delta;
-    Slab S;
-    S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
-    S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-    S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+    Q.S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
+    Q.S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+    Q.S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
 #if HRT_SLAB_FMA
-    S.lo = S.lo * S.inv;
-    S.hi = S.hi * S.inv;
+    Q.S.lo = Q.S.lo * Q.S.inv;
+    Q.S.hi = Q.S.hi * Q.S.inv;
 #endif
+    Q.node = P.bvh_root;
+    return true;
+}
 
+// The walk. Returns true when it has finished; with SUSPEND it may return false after a pop, once fewer
+// than `below` lanes of the wave are still walking (every call makes progress: the check follows a pop).
+template <bool SUSPEND>
+__device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
+                                        Tally& tally, uint32_t below) {
     const float4* __restrict__ nodes = P.bvh_nodes;
-    uint32_t node = P.bvh_root;
-    int sp = 0;
-    bool overflow = false;
+    const Slab S = Q.S;
+    const float a4 = Q.a4, a2 = Q.a2;
+    uint32_t node = Q.node;
+    int sp = Q.sp;
+    float bt = Q.bt;
+    int bc = Q.bc;
+    // overflow and finished are kept as integers (VGPRs): an i1 lane mask carried through the nested
+    // divergent loops of k_trace_split was observed to keep stale overflow bits (sticky full scans)
+    uint32_t overflow = 0u, finished = 0u;
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
             const float4 n0 = nodes[4 * node + 0];
@@ -288,7 +323,7 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
                     stack[sp * 256] = lfirst ? right : left;
                     sp++;
                 } else {
-                    overflow = true;
+                    overflow = 1u;
                 }
                 node = lfirst ? left : right;
                 continue;
@@ -300,20 +335,47 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
             for (uint32_t j = 0; j < cnt; j++) {
                 const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
                 if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
-                    if (t < bt || (bc >= 0 && P.bvh_slot[first + j] < slot_of(bc))) { bt = t; bc = (int)(first + j); }
+                    if (t < bt || (bc >= 0 && P.bvh_slot[first + j] < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                 }
             }
             tally.spheres += cnt;
         }
-        if (sp == 0) break;
+        if (sp == 0) {
+            finished = 1u;
+            break;
+        }
         node = stack[(--sp) * 256];
+        if constexpr (SUSPEND) {
+            if ((uint32_t)__popcll(__ballot(1)) < below) break;
+        }
     }
-    if (overflow) {
+    Q.node = node;
+    Q.sp = sp;
+    Q.bt = bt;
+    Q.bc = bc;
+    Q.full_scan |= overflow;
+#ifdef HRT_DEBUG_SPLIT
+    if (overflow) atomicAdd(P.counter + 6, 1ull);
+    if (sp > 12) atomicAdd(P.counter + 7, 1ull);
+#endif
+    return finished != 0u;
+}
+
+__device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const BvhQuery& Q, float& best,
+                                       Tally& tally) {
+    if (Q.full_scan != 0u) {
         tally.spheres += P.nslots;
         return scan_spheres(P, r, best);
     }
-    best = bt;
-    return bc >= 0 ? slot_of(bc) : -1;
+    best = Q.bt;
+    return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
+}
+
+__device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
+                                                Tally& tally) {
+    BvhQuery Q;
+    if (bvh_begin(P, r, best, Q, tally)) bvh_run<false>(P, r, Q, stack, tally, 0u);
+    return bvh_end(P, r, Q, best, tally);
 }
 
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
@@ -453,7 +515,7 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
     const float4* __restrict__ nodes = P.tb_nodes;
     uint32_t node = P.tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
     int sp = 0;
-    bool overflow = false;
+    uint32_t overflow = 0u;  // an integer, not an i1 lane mask (see bvh_run)
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
             const float4 n0 = nodes[4 * node + 0];
@@ -471,7 +533,7 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
                     stack[sp * 256] = lfirst ? right : left;
                     sp++;
                 } else {
-                    overflow = true;
+                    overflow = 1u;
                 }
                 node = lfirst ? left : right;
                 continue;
@@ -493,7 +555,7 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
         if (sp == 0) break;
         node = stack[(--sp) * 256];
     }
-    if (overflow) {  // a dropped subtree: finish with the lexicographic minimum over every triangle
+    if (overflow != 0u) {  // a dropped subtree: finish with the lexicographic minimum over every triangle
         for (uint32_t j = 0; j < P.m; j++) {
             const float t = tri_t(r, P.tris[j]);
             if (t >= 1e-4f && (t < best || (t == best && bj >= 0 && (int)j < bj))) {
@@ -974,6 +1036,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
     }
 }
 
+// Sample queue with suspendable walks (sphere program, culling BVH; rt_params.suspend_below > 0).
+// In k_trace a wave's query step lasts as long as its slowest lane's walk: secondary rays of one wave
+// take very different paths through the tree, so most lanes idle at the end of every step (PMC of
+// k_trace on C3: 26 of 64 lanes active per VALU instruction). Here the walk is suspended, state kept
+// (BvhQuery in registers, stack in LDS), as soon as fewer than `suspend_below` lanes of the wave are still
+// walking; the finished lanes shade, start their next query (or sample) and all lanes walk on together.
+// Every lane computes exactly the same query as k_trace, so the sample colours are bit-identical.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split(const KParams P) {
+    constexpr int MODE = MODE_SPHERE;
+    const uint32_t lane = threadIdx.x & 63u;
+    __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+    uint32_t* const stack = bvh_stack + threadIdx.x;
+    Tally tally;
+    uint32_t queries = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const uint32_t suspend_below = P.suspend_below;
+
+    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    bool drained = false;
+    Ray ray;
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    float sky_t = 0.0f;
+    uint32_t s = 0, bounce = 0, pix = 0, fl = 0;
+    bool have = false;
+    uint32_t qs = 0;  // query state of the lane's sample: 0 start a query, 1 walking, 2 walk finished
+    BvhQuery Q;
+    while (true) {
+        bool need = !have && !drained;
+        unsigned long long m = __ballot(need);
+        while (m != 0ull) {
+            if (job_next == job_total) {
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                j = __shfl(j, 0);
+                if (j >= P.njobs) {
+                    drained = true;
+                    break;
+                }
+                const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                job_tile = (uint32_t)(j / P.nchunks);
+                job_f0 = chunk * P.job_frames;
+                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
+                job_next = 0;
+            }
+            const uint32_t avail = job_total - job_next;
+            const uint32_t rank = (uint32_t)__popcll(m & below);
+            if (need && rank < avail) {
+                const uint32_t sid = job_next + rank;
+                const uint32_t l = sid & 63u;
+                fl = job_f0 + (sid >> 6);
+                pix = job_tile * 64u + l;
+                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
+                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
+                need = false;
+                if (x < P.W && kr < P.nrows) {
+                    const uint32_t y = P.row0 + kr * P.row_step;
+                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
+                    sky_t = ray.d.y * 0.5f + 0.5f;
+                    att = mk(1.0f, 1.0f, 1.0f);
+                    bounce = 0;
+                    have = true;
+                    qs = 0;
+                }
+            }
+            const uint32_t took = min((uint32_t)__popcll(m), avail);
+            job_next += took;
+            m = __ballot(need);
+        }
+        if (drained && __ballot(have) == 0ull) break;
+        if (have && qs == 0u) {
+            if (bounce < P.bounces) {
+                qs = bvh_begin(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+            } else {  // bounce cap 0: the sample is the sky colour
+                qs = 3u;
+            }
+        }
+        if (have && qs == 1u) {
+            if (bvh_run<true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
+        }
+        if (have && qs >= 2u) {
+            bool done = true;
+            if (qs == 2u) {
+                float best = FLT_MAX_REF;
+                const int bi = bvh_end(P, ray, Q, best, tally);
+                queries++;
+                if (bi >= 0) {
+                    Hit h;
+                    sphere_record(P, ray, bi, best, h);
+                    scatter<MODE>(s, ray, h);
+                    att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                    bounce++;
+                    done = bounce >= P.bounces;
+                }
+            }
+            if (done) {
+                const float u = 1.0f - sky_t;
+                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+                const f3 c = att * sky;
+                float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
+                o[0] = c.x;
+                o[1] = c.y;
+                o[2] = c.z;
+                have = false;
+            }
+            qs = 0u;
+        }
+    }
+    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+    }
+}
+
 // Folds P.nframes sample colours per pixel into the image, in frame order, with the same expression
 // k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per tile-padded pixel, in the buffer's
 // tile-major order, so the frame-major colour reads are contiguous across the wave.
@@ -1036,7 +1218,9 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {
     if (P.njobs == 0) return hipSuccess;
     switch (mode) {
-    case MODE_SPHERE: return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
+    case MODE_SPHERE:
+        if (variant == SCAN_BVH && P.suspend_below > 0u) return launch_persistent(k_trace_split, P, stream);
+        return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
     case MODE_TRIS:
         return P.tri_bvh ? launch_trace_mode<MODE_TRIS, true>(variant, P, stream)
                          : launch_trace_mode<MODE_TRIS, false>(variant, P, stream);

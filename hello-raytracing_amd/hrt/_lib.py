@@ -41,6 +41,7 @@ class RtParams(C.Structure):
         ("queue_budget_mb", C.c_uint32),
         ("job_frames", C.c_uint32),
         ("tri_bvh", C.c_uint32),
+        ("suspend_below", C.c_uint32),
     ]
 
 

@@ -51,7 +51,7 @@ def test_struct_layouts_match_header():
     for py, name in ((hrt.RtParams, "rt_params"), (hrt.RtStats, "rt_stats")):
         fields = _header_struct(name)
         assert [(f, ctypes_of[t]) for t, f in fields] == list(py._fields_), name
-    assert C.sizeof(hrt.RtParams) == 11 * 4
+    assert C.sizeof(hrt.RtParams) == 12 * 4
     assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]

@@ -241,6 +241,38 @@ def test_scan_variants_bit_identical(variant, schedule):
         assert r.stats().queries == q
 
 
+@pytest.mark.parametrize("suspend_below", [1, 24, 48, 64])
+def test_suspendable_walks_bit_identical(suspend_below):
+    """k_trace_split (walks suspended below `suspend_below` walking lanes, finished lanes refilled) gives the
+    oracle's bits, ray counts and the same box/sphere test counts as k_trace; also with the 0-bounce cap and
+    a ragged image (partial 8x8 tiles)."""
+    for sd in (scenes.config_c3(190, 106, 5), scenes.golden_scene("dielectric_materials", 128, 128),
+               scenes.golden_scene("complex_scene", 100, 70)):
+        sd.frames = 5
+        if sd.name.startswith("complex"):
+            sd.min_sphere_slots = 0
+            sd.spheres = np.concatenate([sd.spheres] * 8)  # >= 32 slots: the culling BVH runs
+        counts = []
+        for sb in (0, suspend_below):
+            r = scenes.make_renderer(sd)
+            r.set_params(variant=4, schedule=2, suspend_below=sb)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            counts.append((st.queries, st.box_tests, st.sphere_tests))
+            img = r.read_image()
+        ref, q = scenes.oracle_render(sd)
+        assert_parity(img, ref, f"{sd.name} suspend_below {suspend_below}")
+        assert counts[0] == counts[1] and counts[1][0] == q
+    sd = scenes.config_c3(64, 40, 3)
+    sd.bounces = 0
+    r = scenes.make_renderer(sd)
+    r.set_params(variant=4, schedule=2, suspend_below=suspend_below)
+    r.draw_frames(sd.frames, 1000, 10)
+    ref, q = scenes.oracle_render(sd)
+    assert_parity(r.read_image(), ref, "C3 0 bounces")
+    assert r.stats().queries == q == 0
+
+
 def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
