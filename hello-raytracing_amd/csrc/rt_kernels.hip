@@ -158,7 +158,18 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
 struct Tally {
     uint32_t boxes = 0, spheres = 0;  // sphere culling BVH box tests, ray-sphere tests
     uint32_t nodes = 0, tris = 0;     // triangle program: implicit-heap node tests, triangle tests
+#ifdef HRT_STAMPS
+    // diagnostic build, k_trace_split: lane and wave counts of walk steps (internal node / leaf), rounds,
+    // lanes shading per round, rounds with a shading lane
+    uint32_t lbox = 0, wbox = 0, lleaf = 0, wleaf = 0, rounds = 0, lshade = 0, wshade = 0;
+#endif
 };
+
+#ifdef HRT_STAMPS
+__device__ __forceinline__ bool first_active_lane() {
+    return __lane_id() == (unsigned)(__ffsll((unsigned long long)__ballot(1)) - 1);
+}
+#endif
 
 // (t, slot) lexicographic minimum = the reference's linear scan: strict `t < best` keeps the first slot
 // among equal t, so a later-visited lower slot with the same t must win.
@@ -293,7 +304,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
 
 // The walk. Returns true when it has finished; with SUSPEND it may return false after a pop, once fewer
 // than `below` lanes of the wave are still walking (every call makes progress: the check follows a pop).
-template <bool SUSPEND>
+template <bool SUSPEND, int STACK = BVH_STACK>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below) {
     const float4* __restrict__ nodes = P.bvh_nodes;
@@ -308,6 +319,12 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
     uint32_t overflow = 0u, finished = 0u;
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
+#ifdef HRT_STAMPS
+            if constexpr (SUSPEND) {
+                tally.lbox++;
+                if (first_active_lane()) tally.wbox++;
+            }
+#endif
             const float4 n0 = nodes[4 * node + 0];
             const float4 n1 = nodes[4 * node + 1];
             const float4 n2 = nodes[4 * node + 2];
@@ -319,7 +336,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
-                if (sp < BVH_STACK) {
+                if (sp < STACK) {
                     stack[sp * 256] = lfirst ? right : left;
                     sp++;
                 } else {
@@ -331,6 +348,12 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             if (hl) { node = left; continue; }
             if (hr) { node = right; continue; }
         } else {
+#ifdef HRT_STAMPS
+            if constexpr (SUSPEND) {
+                tally.lleaf++;
+                if (first_active_lane()) tally.wleaf++;
+            }
+#endif
             const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
             for (uint32_t j = 0; j < cnt; j++) {
                 const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
@@ -1043,10 +1066,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
 // (BvhQuery in registers, stack in LDS), as soon as fewer than `suspend_below` lanes of the wave are still
 // walking; the finished lanes shade, start their next query (or sample) and all lanes walk on together.
 // Every lane computes exactly the same query as k_trace, so the sample colours are bit-identical.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split(const KParams P) {
+// 7 waves per SIMD (72-VGPR budget, no spills) with a 20-entry stack (20 KB of LDS per workgroup; 24 entries
+// would cap the CU at 6 workgroups): measured +1.6 % over 6 waves on C3; 8 waves spill (-10 %).
+constexpr int SPLIT_STACK = 20;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t bvh_stack[BVH_STACK * 256];
+    __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
@@ -1105,6 +1131,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             m = __ballot(need);
         }
         if (drained && __ballot(have) == 0ull) break;
+#ifdef HRT_STAMPS
+        if (lane == 0) tally.rounds++;
+#endif
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
                 qs = bvh_begin(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
@@ -1113,9 +1142,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
         }
         if (have && qs == 1u) {
-            if (bvh_run<true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
+            if (bvh_run<true, SPLIT_STACK>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
         }
         if (have && qs >= 2u) {
+#ifdef HRT_STAMPS
+            tally.lshade++;
+            if (first_active_lane()) tally.wshade++;
+#endif
             bool done = true;
             if (qs == 2u) {
                 float best = FLT_MAX_REF;
@@ -1143,6 +1176,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             qs = 0u;
         }
     }
+#ifdef HRT_STAMPS
+    {
+        unsigned long long v[7] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
+                                   tally.wshade};
+#pragma unroll
+        for (int c = 0; c < 7; c++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
+        }
+        if (lane == 0)
+            for (int c = 0; c < 7; c++) atomicAdd(P.counter + 5 + c, v[c]);
+    }
+#endif
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {

@@ -244,8 +244,9 @@ def test_scan_variants_bit_identical(variant, schedule):
 @pytest.mark.parametrize("suspend_below", [1, 24, 48, 64])
 def test_suspendable_walks_bit_identical(suspend_below):
     """k_trace_split (walks suspended below `suspend_below` walking lanes, finished lanes refilled) gives the
-    oracle's bits, ray counts and the same box/sphere test counts as k_trace; also with the 0-bounce cap and
-    a ragged image (partial 8x8 tiles)."""
+    oracle's bits and ray counts; also with the 0-bounce cap and a ragged image (partial 8x8 tiles). Its
+    box/sphere test counts may differ from k_trace's (parked leaves are tested later, against a larger
+    best t), never its results."""
     for sd in (scenes.config_c3(190, 106, 5), scenes.golden_scene("dielectric_materials", 128, 128),
                scenes.golden_scene("complex_scene", 100, 70)):
         sd.frames = 5
@@ -262,7 +263,7 @@ def test_suspendable_walks_bit_identical(suspend_below):
             img = r.read_image()
         ref, q = scenes.oracle_render(sd)
         assert_parity(img, ref, f"{sd.name} suspend_below {suspend_below}")
-        assert counts[0] == counts[1] and counts[1][0] == q
+        assert counts[0][0] == counts[1][0] == q
     sd = scenes.config_c3(64, 40, 3)
     sd.bounces = 0
     r = scenes.make_renderer(sd)
