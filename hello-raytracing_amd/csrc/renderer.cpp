@@ -383,7 +383,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
             P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
-            P.suspend_below = r->mode == RT_MODE_SPHERE ? r->params.suspend_below : 0u;
+            P.suspend_below = P.tri_bvh ? 0u : r->params.suspend_below;  // the opt-in SAH walk is not split
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
             P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
@@ -485,7 +485,9 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.schedule = RT_SCHEDULE_AUTO;
     r->params.queue_budget_mb = 4096;
     r->params.job_frames = 8;
-    r->params.suspend_below = 16;  // measured on C3: 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s
+    // measured: C3 (sphere) 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s;
+    //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92
+    r->params.suspend_below = mode == RT_MODE_SPHERE ? 16u : 32u;
     if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
         rt_destroy(r);

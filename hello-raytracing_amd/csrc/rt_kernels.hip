@@ -513,6 +513,74 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, float& 
     }
 }
 
+// The same walk, split for k_trace_split_tris: heap_begin / heap_run (suspendable: returns false once
+// fewer than `below` lanes of the wave are still walking, after a flush, so no deferred triangle is
+// pending) with the walk state in HeapWalk. The walk, its step cap and the order of the triangle tests
+// are unchanged, so the winner and the node/triangle counts are those of walk_bvh.
+struct HeapWalk {
+    f3 inv;           // 1 / d, the value intersect_node recomputes per node
+    uint32_t i, step;
+    float best;       // starts at the sphere winner's t (triangles must beat it: `t >= best` rejects)
+    int bj;           // winning triangle (-1: none)
+};
+
+__device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W) {
+    W.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    W.i = 1u;
+    W.step = 0u;
+    W.best = best;
+    W.bj = -1;
+}
+
+template <bool SUSPEND>
+__device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand,
+                                         uint32_t below) {
+    const f3 inv = W.inv;
+    const uint32_t n = P.n, m = P.m;
+    uint32_t i = W.i, step = W.step, nc = 0u;
+    uint32_t walking = 1u;  // an integer, not an i1 lane mask (see bvh_run)
+    float best = W.best;
+    int bj = W.bj;
+    while (true) {
+        while (walking != 0u && __ballot(nc == TRI_BATCH) == 0ull) {
+            bool advance = true;
+            if (i < n) {
+                tally.nodes++;
+                if (node_hit(P, i, r.o, inv)) {
+                    i *= 2u;
+                    advance = false;
+                }
+            } else {
+                const uint32_t j = i - n;
+                if (j >= m) {
+                    walking = 0u;
+                    advance = false;
+                } else {
+                    tally.tris++;
+                    cand[(nc++) * 256u] = j;
+                }
+            }
+            if (advance) {
+                i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
+                if (i == 0u) walking = 0u;
+                i++;
+            }
+            if (++step == 600u) walking = 0u;  // the reference's step cap
+        }
+        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
+        nc = 0u;
+        if (walking == 0u) break;
+        if constexpr (SUSPEND) {
+            if ((uint32_t)__popcll(__ballot(1)) < below) break;
+        }
+    }
+    W.i = i;
+    W.step = step;
+    W.best = best;
+    W.bj = bj;
+    return walking == 0u;
+}
+
 // Opt-in triangle walk (rt_params.tri_bvh = 1; host/tri_bvh.hpp): an ordered, culling stack walk of a
 // binned-SAH BVH2 with the same Moller-Trumbore arithmetic, keeping the (t, triangle index)
 // lexicographic minimum — the winner of the reference's ordered walk, which reaches leaves in increasing
@@ -1202,6 +1270,145 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     }
 }
 
+// Sample queue with suspendable walks for the triangle and mixed programs (reference heap walk; the
+// sphere part of the mixed program is the linear scan `SCAN`, simple or deferred). A lane's query goes
+// begin (sphere scan) -> heap walk -> shade; the wave suspends the walks once fewer than
+// `suspend_below` lanes are still walking, so lanes whose rays miss the mesh (one node test) do not idle
+// behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s). Bit-identical to k_trace, with the same
+// node/triangle counts. (The mixed program with the culling BVH stays on k_trace: a two-phase split,
+// sphere walk then heap walk, measured slower on C5.)
+template <int MODE, int SCAN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split_tris(const KParams P) {
+    static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
+    static_assert(SCAN != SCAN_BVH, "the mixed program with the culling BVH runs k_trace");
+    const uint32_t lane = threadIdx.x & 63u;
+    __shared__ uint32_t tri_list[TRI_BATCH * 256];  // per-lane deferred-triangle list
+    uint32_t* const cand = tri_list + threadIdx.x;
+    uint16_t* defer_list = nullptr;
+    if constexpr (SCAN == SCAN_DEFER) {
+        __shared__ uint16_t defer_cand[(CAND_CAP + 1) * 256];
+        defer_list = defer_cand + threadIdx.x;
+    }
+    Tally tally;
+    uint32_t queries = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const uint32_t suspend_below = P.suspend_below;
+
+    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    bool drained = false;
+    Ray ray;
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    float sky_t = 0.0f;
+    uint32_t s = 0, bounce = 0, pix = 0, fl = 0;
+    bool have = false;
+    // query state: 0 start, 3 heap walk, 4 shade, 5 sky only
+    uint32_t qs = 0;
+    int bi = -1;  // sphere winner slot
+    HeapWalk W;
+    while (true) {
+        bool need = !have && !drained;
+        unsigned long long m = __ballot(need);
+        while (m != 0ull) {
+            if (job_next == job_total) {
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                j = __shfl(j, 0);
+                if (j >= P.njobs) {
+                    drained = true;
+                    break;
+                }
+                const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                job_tile = (uint32_t)(j / P.nchunks);
+                job_f0 = chunk * P.job_frames;
+                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
+                job_next = 0;
+            }
+            const uint32_t avail = job_total - job_next;
+            const uint32_t rank = (uint32_t)__popcll(m & below);
+            if (need && rank < avail) {
+                const uint32_t sid = job_next + rank;
+                const uint32_t l = sid & 63u;
+                fl = job_f0 + (sid >> 6);
+                pix = job_tile * 64u + l;
+                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
+                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
+                need = false;
+                if (x < P.W && kr < P.nrows) {
+                    const uint32_t y = P.row0 + kr * P.row_step;
+                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
+                    sky_t = ray.d.y * 0.5f + 0.5f;
+                    att = mk(1.0f, 1.0f, 1.0f);
+                    bounce = 0;
+                    have = true;
+                    qs = 0;
+                }
+            }
+            const uint32_t took = min((uint32_t)__popcll(m), avail);
+            job_next += took;
+            m = __ballot(need);
+        }
+        if (drained && __ballot(have) == 0ull) break;
+        if (have && qs == 0u) {
+            if (bounce >= P.bounces) {
+                qs = 5u;  // bounce cap 0: the sample is the sky colour
+            } else if constexpr (MODE == MODE_TRIS) {
+                bi = -1;
+                heap_begin(ray, FLT_MAX_REF, W);
+                qs = 3u;
+            } else {
+                float sb = FLT_MAX_REF;
+                if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
+                else bi = scan_spheres(P, ray, sb);
+                tally.spheres += P.nslots;
+                heap_begin(ray, sb, W);
+                qs = 3u;
+            }
+        }
+        if (have && qs == 3u) {
+            if (heap_run<true>(P, ray, W, tally, cand, suspend_below)) qs = 4u;
+        }
+        if (have && qs >= 4u) {
+            bool done = true;
+            if (qs == 4u) {
+                queries++;
+                Hit h;
+                bool hit = true;
+                if (W.bj >= 0) tri_record(P, ray, P.tris[W.bj], W.best, h);
+                else if (bi >= 0) sphere_record(P, ray, bi, W.best, h);
+                else hit = false;
+                if (hit) {
+                    scatter<MODE>(s, ray, h);
+                    att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                    bounce++;
+                    done = bounce >= P.bounces;
+                }
+            }
+            if (done) {
+                const float u = 1.0f - sky_t;
+                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+                const f3 c = att * sky;
+                float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
+                o[0] = c.x;
+                o[1] = c.y;
+                o[2] = c.z;
+                have = false;
+            }
+            qs = 0u;
+        }
+    }
+    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 5; c++)
+            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+    }
+}
+
 // Folds P.nframes sample colours per pixel into the image, in frame order, with the same expression
 // k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per tile-padded pixel, in the buffer's
 // tile-major order, so the frame-major colour reads are contiguous across the wave.
@@ -1252,6 +1459,18 @@ static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stre
 // variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host); P.tri_bvh picks the triangle walk.
 template <int MODE, bool TSAH>
 static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t stream) {
+    if constexpr (MODE != MODE_SPHERE && !TSAH) {
+        if (P.suspend_below > 0u) {
+            if constexpr (MODE == MODE_TRIS) {
+                return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
+            } else {
+                if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
+                if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream);
+                // mixed program with the culling BVH (C5): the two-phase split measured slower than k_trace
+                // (256-spp C5: 6.10 Grays/s unsplit; 5.93 both phases split at 16, 6.05 heap walk only)
+            }
+        }
+    }
     if constexpr (MODE == MODE_TRIS) {
         return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream);
     } else {

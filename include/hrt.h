@@ -74,10 +74,12 @@ typedef struct rt_params {
                                   parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
                                   same closest hit except where the reference's 600-step cap or
                                   unpadded slab tests drop a triangle (non-parity)  */
-    uint32_t suspend_below;    /* sample queue, sphere program with the culling BVH (variant 4): a wave
-                                  suspends its walks once fewer than this many of its 64 lanes are still
-                                  walking, so finished lanes shade and start their next query instead of
-                                  idling (0 = every query runs to completion, k_trace); default 16.
+    uint32_t suspend_below;    /* sample queue: a wave suspends its walks (sphere culling BVH of the sphere
+                                  program; reference heap walk of the triangle / mixed programs) once
+                                  fewer than this many of its 64 lanes are still walking, so finished
+                                  lanes shade and start their next query instead of idling (0 = every
+                                  query runs to completion, k_trace); default 16 (sphere) / 32 (others);
+                                  not used by the mixed program with the culling BVH or tri_bvh = 1.
                                   Bit-identical either way                      */
 } rt_params;
 

@@ -274,6 +274,37 @@ def test_suspendable_walks_bit_identical(suspend_below):
     assert r.stats().queries == q == 0
 
 
+@pytest.mark.parametrize("variant", [1, 3, 4])
+def test_suspendable_heap_walk_bit_identical(variant):
+    """k_trace_split_tris (mixed program: sphere scan `variant`, then the reference heap walk, suspendable)
+    gives the oracle's bits and ray counts, and k_trace's node/triangle test counts (the walk itself is
+    unchanged); the triangle program on Suzanne and the dragon likewise. Variant 4 (culling BVH) keeps
+    k_trace whatever suspend_below says."""
+    sd = scenes.config_c4(96, 72, 4)
+    if variant == 4:
+        sd.spheres = np.concatenate([sd.spheres] + [scenes.rtiow_spheres()[:60]])  # >= 32 slots: culling BVH
+    cases = [(sd, variant)]
+    if variant == 1:  # triangle program: Suzanne, and the dragon (its walks hit the 600-step cap)
+        for builder, w, h in (("new_suzane", 80, 60), ("new_dragon", 64, 48)):
+            scene = getattr(hrt.SceneTris, builder)(w, h)
+            cases.append((scenes.SceneDef(builder, hrt.RT_MODE_TRIS, w, h, scene.camera, bvh=scene.tris_bvh.view(),
+                                          frames=4), 1))
+    for sd, v in cases:
+        counts = []
+        for sb in (0, 1, 16, 48):
+            r = scenes.make_renderer(sd)
+            r.set_params(variant=v if sd.mode != hrt.RT_MODE_TRIS else 0, schedule=2, suspend_below=sb)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            counts.append((st.queries, st.node_tests, st.tri_tests))
+            img = r.read_image()
+            if sb == 16:
+                ref, q = scenes.oracle_render(sd)
+                assert_parity(img, ref, f"{sd.name} variant {v} suspend_below {sb}")
+                assert st.queries == q
+        assert all(c == counts[0] for c in counts), counts
+
+
 def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
