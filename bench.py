@@ -194,6 +194,7 @@ def main() -> int:
     tri_tests = 0
     variant = 0
     schedule = 0
+    suspend = 0
     trace_ms = 0.0
     trace_launches = 0
     for i in range(args.steps):
@@ -207,6 +208,7 @@ def main() -> int:
         tri_tests += st.tri_tests
         variant = st.variant
         schedule = st.schedule
+        suspend = st.suspend_below
         trace_ms += st.trace_ms
         trace_launches += st.trace_launches
         log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernels {st.kernel_ms:.1f} ms (trace {st.trace_ms:.1f}), "
@@ -292,8 +294,11 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": (f"k_trace<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if schedule == 2
-                           else f"k_render<{MODE_NAMES[sd.mode]}, scan variant {variant}>"),
+                "kernel": (f"k_render<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if schedule != 2
+                           else f"k_trace<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if not suspend
+                           else f"k_trace_split (sphere, culling BVH, suspend below {suspend} lanes)"
+                           if sd.mode == 0 else
+                           f"k_trace_split_tris<{MODE_NAMES[sd.mode]}, scan variant {variant}> (suspend below {suspend})"),
                 "schedule": {1: "tiles", 2: "sample-queue"}.get(schedule, str(schedule)),
                 "all_kernels_ms_per_step": round(float(all_t[0, 8]) / args.steps, 3),
                 "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),

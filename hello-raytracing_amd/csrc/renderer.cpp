@@ -131,6 +131,7 @@ struct rt_renderer {
     std::vector<hipEvent_t> ev_trace;  // start/stop pairs around each k_trace launch of the last draw
     uint32_t trace_pairs = 0;
     uint32_t last_schedule = 0;
+    uint32_t last_suspend = 0;
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
@@ -362,6 +363,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     const uint32_t schedule = resolve_schedule(r, count);
     r->last_variant = variant;
     r->last_schedule = schedule;
+    r->last_suspend = 0;
 
     uint32_t launches = 0;
     if (schedule == RT_SCHEDULE_QUEUE) {
@@ -383,7 +385,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
             P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
-            P.suspend_below = P.tri_bvh ? 0u : r->params.suspend_below;  // the opt-in SAH walk is not split
+            // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the
+            // heap walk of the triangle / mixed programs with a linear sphere scan; not the opt-in SAH walk
+            const bool split = !P.tri_bvh && (r->mode == RT_MODE_SPHERE ? variant == hrt_dev::SCAN_BVH
+                                                                         : variant != hrt_dev::SCAN_BVH);
+            P.suspend_below = split ? r->params.suspend_below : 0u;
+            r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
             P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
@@ -445,6 +452,7 @@ int finish_stats(rt_renderer* r) {
     r->stats.tri_tests = q[4];
     r->stats.variant = (uint32_t)r->last_variant;
     r->stats.schedule = r->last_schedule;
+    r->stats.suspend_below = r->last_suspend;
     r->timing_pending = false;
     return RT_OK;
 }

@@ -700,7 +700,10 @@ __device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
     const float y = rng_float(s);
     const float z = rng_float(s);
     const f3 v = normalize(mk(x, y, z));
-    if (length(v) < EPS) return n;
+    // `length(v) < EPSILON` (:110) never holds here, so it is not evaluated: x, y, z are rng floats in
+    // [0, 1]; either all are 0 (v = NaN, and NaN < EPS is false) or the largest is >= 2^-32, dot(v, v) is a
+    // normal float and the normalised v has length >= 0.577. The oracle keeps the test; parity compares.
+    (void)EPS;
     if (dot(v, n) > 0.0f) return v;
     return -v;
 }
@@ -1461,13 +1464,14 @@ template <int MODE, bool TSAH>
 static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t stream) {
     if constexpr (MODE != MODE_SPHERE && !TSAH) {
         if (P.suspend_below > 0u) {
+            // (the host sets suspend_below = 0 for the mixed program with the culling BVH: a two-phase split,
+            // sphere walk then heap walk, measured slower than k_trace on C5 at 256 spp — 6.10 Grays/s
+            // unsplit, 5.93 with both phases split at 16, 6.05 with the heap walk split only)
             if constexpr (MODE == MODE_TRIS) {
                 return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
             } else {
                 if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
                 if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream);
-                // mixed program with the culling BVH (C5): the two-phase split measured slower than k_trace
-                // (256-spp C5: 6.10 Grays/s unsplit; 5.93 both phases split at 16, 6.05 heap walk only)
             }
         }
     }

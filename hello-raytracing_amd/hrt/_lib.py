@@ -60,7 +60,7 @@ class RtStats(C.Structure):
         ("tri_tests", C.c_uint64),
         ("trace_ms", C.c_double),
         ("trace_launches", C.c_uint32),
-        ("pad1", C.c_uint32),
+        ("suspend_below", C.c_uint32),
     ]
 
 

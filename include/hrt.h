@@ -101,7 +101,8 @@ typedef struct rt_stats {
     uint64_t tri_tests;    /* triangle program: Moller-Trumbore tests                                   */
     double trace_ms;       /* HIP-event time of the ray-tracing kernels alone (k_render / k_trace)      */
     uint32_t trace_launches; /* launches of those kernels (the dominant kernel's launch count)          */
-    uint32_t pad1;
+    uint32_t suspend_below; /* walks suspended below this many walking lanes in the last draw (k_trace_split*);
+                              0 = every query ran to completion (k_trace, k_render)                    */
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),
