@@ -305,6 +305,37 @@ def test_suspendable_heap_walk_bit_identical(variant):
         assert all(c == counts[0] for c in counts), counts
 
 
+def test_full_size_headline_configs_agree():
+    """BASELINE sizes (C3 and C4 at 1920x1080, 8 frames; the bench renders 1024 / 512): the default
+    suspendable-walk kernels, plain k_trace and the tiles schedule give the same image bits and ray counts;
+    an 8-way interleaved row partition (the multi-GPU split) reassembles to the full image; and every 90th
+    row matches the CPU oracle bit for bit."""
+    for sd in (scenes.config_c3(1920, 1080, 8), scenes.config_c4(1920, 1080, 8)):
+        runs = []
+        for params in ({}, {"suspend_below": 0}, {"schedule": hrt.RT_SCHEDULE_TILES}):
+            r = scenes.make_renderer(sd)
+            r.set_params(**params)
+            r.draw_frames(sd.frames, 1000, 10)
+            runs.append((r.read_image(), r.stats()))
+        img, st = runs[0]
+        assert st.schedule == hrt.RT_SCHEDULE_QUEUE and st.suspend_below > 0
+        for other, ost in runs[1:]:
+            np.testing.assert_array_equal(img.view(np.uint32), other.view(np.uint32))
+            assert ost.queries == st.queries
+        parts = []
+        for rank in range(8):
+            r = scenes.make_renderer(sd)
+            r.set_params(row0=rank, row_step=8)
+            r.draw_frames(sd.frames, 1000, 10)
+            parts.append(r.read_image())
+        full = np.empty_like(img)
+        for rank in range(8):
+            full[rank::8] = parts[rank]
+        np.testing.assert_array_equal(full.view(np.uint32), img.view(np.uint32))
+        ref, _ = scenes.oracle_render(sd, rows=(45, 90, 12))
+        assert_parity(img[45::90], ref, f"{sd.name} full size, every 90th row")
+
+
 def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
