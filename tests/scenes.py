@@ -256,3 +256,72 @@ def oracle_render(sd: SceneDef, **kw):
                 spheres=sd.spheres, bvh=sd.bvh, bounces=sd.bounces, min_sphere_slots=sd.min_sphere_slots)
     args.update(kw)
     return O.render(**args)
+
+
+# ---- committed oracle fixtures (tests/golden/oracle, made by tests/golden/make_oracle_fixtures.py)
+ORACLE_FIXTURE_DIR = GOLDEN_DIR / "oracle"
+
+
+def _tris_scene(name: str, width: int, height: int, frames: int) -> SceneDef:
+    from hrt import SceneTris
+    if name == "suzane":
+        tree, cam = SceneTris.build_suzane_tree(), SceneTris.suzane_camera()
+    else:  # dragon on the floor (scene_tris.rs:67-92): its walks hit the 600-step cap
+        tree = SceneTris._mesh_on_floor("xyzrgb_dragon_lp_20.obj", Vec3(0.7, 0.7, 0.2))
+        cam = Camera.new(Vec3(0.0, 2.0, 8.0), Vec3(0.0, 0.0, -8.0), 5.6, 0.0, PI * f32(0.3))
+    return SceneDef(name, hrt.RT_MODE_TRIS, width, height, cam, bvh=tree.view(), frames=frames)
+
+
+def oracle_fixture_cases():
+    """name -> (SceneDef, (row0, row_step)): full-width row subsets (rows row0, row0 + step, ... to the
+    bottom, the set a renderer with rt_params.row0/row_step draws) of every BASELINE config and of the
+    golden and triangle scenes, few frames each."""
+    def frames(sd, f):
+        sd.frames = f
+        return sd
+    return {
+        "golden_complex_scene_64": (frames(golden_scene("complex_scene", 64, 64), 10), (0, 1)),
+        "golden_dielectric_64": (frames(golden_scene("dielectric_materials", 64, 64), 10), (0, 1)),
+        "c1": (config_c1(), (2, 15)),
+        "c2": (frames(config_c2(), 2), (7, 90)),
+        "c3": (frames(config_c3(), 2), (13, 180)),
+        "c4": (frames(config_c4(), 2), (17, 180)),
+        "c5": (frames(config_c5(), 1), (29, 540)),
+        "tris_suzane": (_tris_scene("suzane", 160, 120, 3), (1, 4)),
+        "tris_dragon": (_tris_scene("dragon", 96, 72, 2), (0, 3)),
+    }
+
+
+def oracle_fixture_trees():
+    """name -> Tree (host builders) whose bytes are pinned by tests/golden/oracle/trees.json."""
+    from hrt import Material, Mesh, SceneTris, Tree, read_asset
+    lamb = Material.new_lambertian(Vec3(0.5, 0.5, 0.5))
+
+    def one(asset):
+        t = Tree.from_mesh(Mesh.load_obj(read_asset(asset), lamb))
+        t.build()
+        return t
+    return {
+        "cube": lambda: one("cube.obj"),
+        "suzanne": lambda: one("suzanne.obj"),
+        "new_suzane": SceneTris.build_suzane_tree,
+        "dragon_floor": lambda: SceneTris._mesh_on_floor("xyzrgb_dragon_lp_20.obj", Vec3(0.7, 0.7, 0.2)),
+        "lucy_floor": lambda: SceneTris._mesh_on_floor("lucy_lp_20.obj", Vec3(0.4, 0.3, 0.6)),
+    }
+
+
+def tree_digest(tree) -> dict:
+    import hashlib
+    sizes, nodes, tris, mats = tree.view()
+    return {"sizes": list(sizes), "nodes_sha256": hashlib.sha256(nodes.tobytes()).hexdigest(),
+            "tris_sha256": hashlib.sha256(tris.tobytes()).hexdigest(),
+            "mats_sha256": hashlib.sha256(mats.tobytes()).hexdigest()}
+
+
+def load_oracle_fixture(name: str):
+    """(image float32 [rows, W, 3], manifest entry) of a committed oracle fixture."""
+    man = json.loads((ORACLE_FIXTURE_DIR / "manifest.json").read_text())[name]
+    with np.load(ORACLE_FIXTURE_DIR / "images.npz", allow_pickle=False) as z:
+        img = z[name].copy()
+    return img, man
+

@@ -336,6 +336,23 @@ def test_full_size_headline_configs_agree():
         assert_parity(img[45::90], ref, f"{sd.name} full size, every 90th row")
 
 
+@pytest.mark.parametrize("name", sorted(scenes.oracle_fixture_cases()))
+def test_hip_reproduces_oracle_fixtures(name):
+    """The committed oracle outputs (tests/golden/oracle) re-rendered on the GPU through the C-ABI with the
+    same row subset: image bits, ray counts and triangle-program work counts, under the auto schedule and
+    the sample queue (suspendable walks)."""
+    sd, (row0, step) = scenes.oracle_fixture_cases()[name]
+    want, man = scenes.load_oracle_fixture(name)
+    for schedule in (hrt.RT_SCHEDULE_AUTO, hrt.RT_SCHEDULE_QUEUE):
+        r = scenes.make_renderer(sd)
+        r.set_params(row0=row0, row_step=step, schedule=schedule)
+        r.draw_frames(sd.frames, 1000, 10)
+        assert_parity(r.read_image(), want, f"{name} schedule {schedule}")
+        st = r.stats()
+        assert st.queries == man["queries"]
+        assert (st.node_tests, st.tri_tests) == (man["node_tests"], man["tri_tests"])  # heap-walk work
+
+
 def test_scan_variants_agree_at_scale():
     """Packed/interval scan vs simple scan on a larger C3 render (tens of millions of rays)."""
     sd = scenes.config_c3(640, 360, 32)
