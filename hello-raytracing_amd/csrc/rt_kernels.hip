@@ -232,6 +232,19 @@ __device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx,
     return tmin <= tmax;
 }
 
+// padded_box_hit with the best-t bound as a separate compare: tmin <= min(tmax, bt) <=> tmin <= tmax &&
+// tmin <= bt (no NaN here: finite slabs, bt finite), without the per-iteration canonicalize of bt.
+__device__ __forceinline__ bool padded_box_hit_nb(const float4 mn, const float4 mx, const Slab& S, float bt,
+                                                  float& tenter) {
+    const float t0x = __builtin_fmaf(mn.x, S.inv.x, S.lo.x), t1x = __builtin_fmaf(mx.x, S.inv.x, S.hi.x);
+    const float t0y = __builtin_fmaf(mn.y, S.inv.y, S.lo.y), t1y = __builtin_fmaf(mx.y, S.inv.y, S.hi.y);
+    const float t0z = __builtin_fmaf(mn.z, S.inv.z, S.lo.z), t1z = __builtin_fmaf(mx.z, S.inv.z, S.hi.z);
+    const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmax_ieee(fmin_ieee(t0z, t1z), 0.0f));
+    const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmax_ieee(t0z, t1z));
+    tenter = tmin;
+    return tmin <= tmax && tmin <= bt;
+}
+
 // BVH scan, bit-identical to scan_spheres: every sphere the reference could accept lies in a box the
 // padded slab test visits (float-error bound on the discriminant, DESIGN.md §Sphere BVH exactness), every
 // visited sphere is tested with the reference arithmetic, and the winner is the (t, slot) minimum.
@@ -330,23 +343,23 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             const float4 n2 = nodes[4 * node + 2];
             const float4 n3 = nodes[4 * node + 3];
             float tl, tr;
-            const bool hl = padded_box_hit(n0, n1, S, bt, tl);
-            const bool hr = padded_box_hit(n2, n3, S, bt, tr);
+            const bool hl = padded_box_hit_nb(n0, n1, S, bt, tl);
+            const bool hr = padded_box_hit_nb(n2, n3, S, bt, tr);
             tally.boxes += 2;
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
+            // near child first; the far one is pushed when both are visited (select form: +1 % on C3
+            // over a three-way branch, with padded_box_hit_nb)
+            const bool lfirst = hl && (!hr || tl <= tr);
+            const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
             if (hl && hr) {
-                const bool lfirst = tl <= tr;
                 if (sp < STACK) {
-                    stack[sp * 256] = lfirst ? right : left;
+                    stack[sp * 256] = far;
                     sp++;
                 } else {
                     overflow = 1u;
                 }
-                node = lfirst ? left : right;
-                continue;
             }
-            if (hl) { node = left; continue; }
-            if (hr) { node = right; continue; }
+            if (hl || hr) { node = near; continue; }
         } else {
 #ifdef HRT_STAMPS
             if constexpr (SUSPEND) {
