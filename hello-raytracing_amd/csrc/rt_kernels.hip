@@ -1150,10 +1150,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
 // (BvhQuery in registers, stack in LDS), as soon as fewer than `suspend_below` lanes of the wave are still
 // walking; the finished lanes shade, start their next query (or sample) and all lanes walk on together.
 // Every lane computes exactly the same query as k_trace, so the sample colours are bit-identical.
-// 7 waves per SIMD (72-VGPR budget, no spills) with a 20-entry stack (20 KB of LDS per workgroup; 24 entries
-// would cap the CU at 6 workgroups): measured +1.6 % over 6 waves on C3; 8 waves spill (-10 %).
+// A 20-entry stack (20 KB of LDS per workgroup; 24 entries would cap the CU at 6 workgroups). 6 waves per
+// SIMD (80-VGPR budget): the frame-block primary rays (7 VGPRs) measured +3.5 % on C3 at 6 waves over the
+// per-lane primary rays at 7 waves (72 VGPRs), which in turn were +1.6 % over 6; with them 7 waves spill.
 constexpr int SPLIT_STACK = 20;
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     const uint32_t lane = threadIdx.x & 63u;
     __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
@@ -1163,7 +1164,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
-    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
     bool drained = false;
     Ray ray;
     f3 att = mk(1.0f, 1.0f, 1.0f);
@@ -1172,37 +1172,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     bool have = false;
     uint32_t qs = 0;  // query state of the lane's sample: 0 start a query, 1 walking, 2 walk finished
     BvhQuery Q;
+    // Primary rays are generated a frame-block at a time: when the wave's block (one frame of its job's
+    // 8x8 tile) is used up, every lane computes the primary ray of its own pixel for the next frame at
+    // once (all lanes busy), and lanes that need a sample fetch one from the block's owner lane with
+    // cross-lane reads, instead of each freed lane computing its own with a few lanes active.
+    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+    f3 pr_o = mk(0.0f, 0.0f, 0.0f), pr_d = mk(0.0f, 0.0f, 0.0f);
+    uint32_t pr_s = 0, pr_ok = 0;  // this lane's pixel's primary ray for the block, and whether it exists
     while (true) {
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
         while (m != 0ull) {
-            if (job_next == job_total) {
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(P.queue, 1ull);
-                j = __shfl(j, 0);
-                if (j >= P.njobs) {
-                    drained = true;
-                    break;
+            if (blk_next == 64u) {
+                if (blk_f + 1u < job_nf) {
+                    blk_f++;
+                } else {
+                    unsigned long long j = 0;
+                    if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                    j = __shfl(j, 0);
+                    if (j >= P.njobs) {
+                        drained = true;
+                        break;
+                    }
+                    const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                    job_tile = (uint32_t)(j / P.nchunks);
+                    job_f0 = chunk * P.job_frames;
+                    job_nf = min(P.job_frames, P.nframes - job_f0);
+                    blk_f = 0;
                 }
-                const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                job_tile = (uint32_t)(j / P.nchunks);
-                job_f0 = chunk * P.job_frames;
-                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
-                job_next = 0;
-            }
-            const uint32_t avail = job_total - job_next;
-            const uint32_t rank = (uint32_t)__popcll(m & below);
-            if (need && rank < avail) {
-                const uint32_t sid = job_next + rank;
-                const uint32_t l = sid & 63u;
-                fl = job_f0 + (sid >> 6);
-                pix = job_tile * 64u + l;
-                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
-                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
-                need = false;
-                if (x < P.W && kr < P.nrows) {
+                blk_next = 0;
+                const uint32_t x = (job_tile % P.tiles_w) * 8u + (lane & 7u);
+                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (lane >> 3);
+                pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
+                if (pr_ok) {
                     const uint32_t y = P.row0 + kr * P.row_step;
-                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
+                    const Ray pr = primary_ray<MODE>(P, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, pr_s);
+                    pr_o = pr.o;
+                    pr_d = pr.d;
+                }
+            }
+            const uint32_t avail = 64u - blk_next;
+            const uint32_t rank = (uint32_t)__popcll(m & below);
+            const int src = (int)((blk_next + rank) & 63u);
+            const float ox = __shfl(pr_o.x, src), oy = __shfl(pr_o.y, src), oz = __shfl(pr_o.z, src);
+            const float dx = __shfl(pr_d.x, src), dy = __shfl(pr_d.y, src), dz = __shfl(pr_d.z, src);
+            const uint32_t ss = __shfl(pr_s, src), ok = __shfl(pr_ok, src);
+            if (need && rank < avail) {
+                need = false;
+                if (ok) {
+                    ray.o = mk(ox, oy, oz);
+                    ray.d = mk(dx, dy, dz);
+                    s = ss;
+                    fl = job_f0 + blk_f;
+                    pix = job_tile * 64u + (uint32_t)src;
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
                     bounce = 0;
@@ -1210,8 +1232,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     qs = 0;
                 }
             }
-            const uint32_t took = min((uint32_t)__popcll(m), avail);
-            job_next += took;
+            blk_next += min((uint32_t)__popcll(m), avail);
             m = __ballot(need);
         }
         if (drained && __ballot(have) == 0ull) break;
