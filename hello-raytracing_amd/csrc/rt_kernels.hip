@@ -317,7 +317,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
 
 // The walk. Returns true when it has finished; with SUSPEND it may return false after a pop, once fewer
 // than `below` lanes of the wave are still walking (every call makes progress: the check follows a pop).
-template <bool SUSPEND, int STACK = BVH_STACK>
+template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below) {
     const float4* __restrict__ nodes = P.bvh_nodes;
@@ -343,23 +343,40 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             const float4 n2 = nodes[4 * node + 2];
             const float4 n3 = nodes[4 * node + 3];
             float tl, tr;
-            const bool hl = padded_box_hit_nb(n0, n1, S, bt, tl);
-            const bool hr = padded_box_hit_nb(n2, n3, S, bt, tr);
+            // SELECT (k_trace_split): best-t bound as a separate compare (no per-step canonicalize of bt)
+            // and select-form child order, +1 % on C3; the three-way branch below keeps k_trace's mixed
+            // program (C5) free of spills (the select form spilled 12 VGPRs there, -1.5 %).
+            const bool hl = SELECT ? padded_box_hit_nb(n0, n1, S, bt, tl) : padded_box_hit(n0, n1, S, bt, tl);
+            const bool hr = SELECT ? padded_box_hit_nb(n2, n3, S, bt, tr) : padded_box_hit(n2, n3, S, bt, tr);
             tally.boxes += 2;
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
-            // near child first; the far one is pushed when both are visited (select form: +1 % on C3
-            // over a three-way branch, with padded_box_hit_nb)
-            const bool lfirst = hl && (!hr || tl <= tr);
-            const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
-            if (hl && hr) {
-                if (sp < STACK) {
-                    stack[sp * 256] = far;
-                    sp++;
-                } else {
-                    overflow = 1u;
+            if constexpr (SELECT) {
+                const bool lfirst = hl && (!hr || tl <= tr);
+                const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
+                if (hl && hr) {
+                    if (sp < STACK) {
+                        stack[sp * 256] = far;
+                        sp++;
+                    } else {
+                        overflow = 1u;
+                    }
                 }
+                if (hl || hr) { node = near; continue; }
+            } else {
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < STACK) {
+                        stack[sp * 256] = lfirst ? right : left;
+                        sp++;
+                    } else {
+                        overflow = 1u;
+                    }
+                    node = lfirst ? left : right;
+                    continue;
+                }
+                if (hl) { node = left; continue; }
+                if (hr) { node = right; continue; }
             }
-            if (hl || hr) { node = near; continue; }
         } else {
 #ifdef HRT_STAMPS
             if constexpr (SUSPEND) {
@@ -825,6 +842,79 @@ __device__ __forceinline__ LaneLists lane_lists() {
     return L;
 }
 
+// Refill with primary rays by frame block (k_trace with the simple sphere scan): when the wave's block
+// (one frame of its job's 8x8 tile) is used up, every lane computes the primary ray of its own pixel for
+// the next frame at once (all lanes busy), and lanes that need a sample fetch one from the block's owner
+// lane with cross-lane reads, instead of each freed lane computing its own with a few lanes active
+// (k_trace_split does the same inline).
+struct BlockQueue {
+    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+    f3 pr_o = {0.0f, 0.0f, 0.0f}, pr_d = {0.0f, 0.0f, 0.0f};
+    uint32_t pr_s = 0, pr_ok = 0;  // this lane's pixel's primary ray for the block, and whether it exists
+};
+
+// Free lanes (!have) take the next samples; sets drained once the job queue is empty.
+template <int MODE>
+__device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bool& drained, uint32_t lane,
+                                             unsigned long long below, bool& have, Ray& ray, f3& att,
+                                             float& sky_t, uint32_t& s, uint32_t& bounce, uint32_t& pix,
+                                             uint32_t& fl) {
+    bool need = !have && !drained;
+    unsigned long long m = __ballot(need);
+    while (m != 0ull) {
+        if (B.blk_next == 64u) {
+            if (B.blk_f + 1u < B.job_nf) {
+                B.blk_f++;
+            } else {
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                j = __shfl(j, 0);
+                if (j >= P.njobs) {
+                    drained = true;
+                    break;
+                }
+                const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                B.job_tile = (uint32_t)(j / P.nchunks);
+                B.job_f0 = chunk * P.job_frames;
+                B.job_nf = min(P.job_frames, P.nframes - B.job_f0);
+                B.blk_f = 0;
+            }
+            B.blk_next = 0;
+            const uint32_t x = (B.job_tile % P.tiles_w) * 8u + (lane & 7u);
+            const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
+            B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
+            if (B.pr_ok) {
+                const uint32_t y = P.row0 + kr * P.row_step;
+                const Ray pr = primary_ray<MODE>(P, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
+                B.pr_o = pr.o;
+                B.pr_d = pr.d;
+            }
+        }
+        const uint32_t avail = 64u - B.blk_next;
+        const uint32_t rank = (uint32_t)__popcll(m & below);
+        const int src = (int)((B.blk_next + rank) & 63u);
+        const float ox = __shfl(B.pr_o.x, src), oy = __shfl(B.pr_o.y, src), oz = __shfl(B.pr_o.z, src);
+        const float dx = __shfl(B.pr_d.x, src), dy = __shfl(B.pr_d.y, src), dz = __shfl(B.pr_d.z, src);
+        const uint32_t ss = __shfl(B.pr_s, src), ok = __shfl(B.pr_ok, src);
+        if (need && rank < avail) {
+            need = false;
+            if (ok) {
+                ray.o = mk(ox, oy, oz);
+                ray.d = mk(dx, dy, dz);
+                s = ss;
+                fl = B.job_f0 + B.blk_f;
+                pix = B.job_tile * 64u + (uint32_t)src;
+                sky_t = ray.d.y * 0.5f + 0.5f;
+                att = mk(1.0f, 1.0f, 1.0f);
+                bounce = 0;
+                have = true;
+            }
+        }
+        B.blk_next += min((uint32_t)__popcll(m), avail);
+        m = __ballot(need);
+    }
+}
+
 }  // namespace
 
 // Tiles schedule (rt_params.schedule = RT_SCHEDULE_TILES): one launch = P.nframes frames over this
@@ -1001,6 +1091,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
 
     // wave-uniform job state
     uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    BlockQueue BQ;  // frame-block refill (simple sphere scan only)
     bool drained = false;
     // lane state
     Ray ray;
@@ -1019,7 +1110,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
         st_ta = hrt_stamp();
 #endif
         // refill: free lanes take the next samples of the wave's job, fetching jobs as they run out
+        // frame-block primary rays for the simple sphere scan (C2: 51.8 -> 59.5 Grays/s); the other
+        // instantiations have no registers to spare for the block's 7 values
+        constexpr bool BLOCK_REFILL = MODE == MODE_SPHERE && SCAN == SCAN_SIMPLE;
         bool need = !have && !drained;
+        if constexpr (BLOCK_REFILL) {
+            refill_block<MODE>(P, BQ, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
+            need = false;
+        }
         unsigned long long m = __ballot(need);
         while (m != 0ull) {
             if (job_next == job_total) {
@@ -1247,7 +1345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
         }
         if (have && qs == 1u) {
-            if (bvh_run<true, SPLIT_STACK>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
+            if (bvh_run<true, SPLIT_STACK, true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
         }
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
