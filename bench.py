@@ -102,7 +102,8 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--frames-per-launch", type=int, default=1024, help="tiles schedule: frames per launch")
     ap.add_argument("--schedule", type=int, default=0, help="0 auto (queue), 1 tiles, 2 sample queue")
-    ap.add_argument("--job-frames", type=int, default=8, help="sample queue: frames per 8x8-tile job")
+    ap.add_argument("--job-frames", type=int, default=None, help="sample queue: frames per 8x8-tile job "
+                                                                 "(default: the library's)")
     ap.add_argument("--suspend-below", type=int, default=None,
                     help="sample queue, sphere BVH: suspend a wave's walks below this many walking lanes "
                          "(default: the library's)")
@@ -154,8 +155,10 @@ def main() -> int:
     nslots = len(sd.spheres)
     r = scenes.make_renderer(sd)
     extra = {} if args.suspend_below is None else {"suspend_below": args.suspend_below}
+    if args.job_frames is not None:
+        extra["job_frames"] = args.job_frames
     r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
-                 schedule=args.schedule, job_frames=args.job_frames, tri_bvh=args.tri_bvh, **extra)
+                 schedule=args.schedule, tri_bvh=args.tri_bvh, **extra)
     local_rows = r.local_rows
     max_rows = (sd.height + world - 1) // world
     part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
@@ -325,7 +328,7 @@ def main() -> int:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)
             ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
-                             job_frames=args.job_frames, tri_bvh=args.tri_bvh)
+                             tri_bvh=args.tri_bvh, **extra)
             ref_r.draw_frames(sd.frames, 1000, 10)
             ref_img = torch.from_numpy(ref_r.read_image())
             same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))

@@ -492,10 +492,13 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
     r->params.queue_budget_mb = 4096;
-    r->params.job_frames = 8;
-    // measured: C3 (sphere) 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s;
+    // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
+    // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
+    r->params.job_frames = 16;
+    // measured: C3 (sphere) 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s (first split
+    //           kernel); with the frame-block refill and 16-frame jobs 16 -> 25.2, 24 -> 25.9, 32 -> 25.2;
     //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92
-    r->params.suspend_below = mode == RT_MODE_SPHERE ? 16u : 32u;
+    r->params.suspend_below = mode == RT_MODE_SPHERE ? 24u : 32u;
     if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
         rt_destroy(r);

@@ -69,7 +69,7 @@ typedef struct rt_params {
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
-    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 8        */
+    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 16       */
     uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
                                   parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
                                   same closest hit except where the reference's 600-step cap or
@@ -78,7 +78,7 @@ typedef struct rt_params {
                                   program; reference heap walk of the triangle / mixed programs) once
                                   fewer than this many of its 64 lanes are still walking, so finished
                                   lanes shade and start their next query instead of idling (0 = every
-                                  query runs to completion, k_trace); default 16 (sphere) / 32 (others);
+                                  query runs to completion, k_trace); default 24 (sphere) / 32 (others);
                                   not used by the mixed program with the culling BVH or tri_bvh = 1.
                                   Bit-identical either way                      */
 } rt_params;

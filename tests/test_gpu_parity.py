@@ -595,6 +595,9 @@ def test_bad_arguments_fail_loudly():
                     np.zeros(1, dtype=hrt.MATERIAL_DTYPE))
     small = np.zeros(10, dtype=np.float32)
     assert hrt.lib().rt_read_image(r._h, small.ctypes.data_as(hrt._lib._PF), small.size) == hrt._lib.RT_ERR_ARG
-    for bad in ({"variant": 2}, {"variant": 9}, {"schedule": 3}, {"tri_bvh": 2}, {"row_step": 0}):
-        with pytest.raises(hrt.RtError):  # removed variants, unknown schedule / tree, empty partition
-            r.set_params(**bad)
+    for bad in ({"variant": 2}, {"variant": 9}, {"schedule": 3}, {"tri_bvh": 2}, {"row_step": 0},
+                {"suspend_below": 65}):
+        with pytest.raises(hrt.RtError):  # removed variants, unknown schedule / tree, empty partition,
+            r.set_params(**bad)           # a suspend threshold above the wave width
+    assert hrt.Renderer(8, 8, hrt.RT_MODE_SPHERE).params.suspend_below == 24  # per-program defaults
+    assert r.params.suspend_below == 32
