@@ -262,12 +262,14 @@ int trace_events(rt_renderer* r, uint32_t pair) {
 }
 
 // schedule 0 = the sample queue (load-balanced at sample granularity), except for
-// draws too small to fill the persistent grid for long (< 4M samples: e.g. one interactive frame, C1),
-// where the tiles kernel's single launch has less fixed cost.
+// draws too small to fill the persistent grid for long (< 1.5 Mi samples: e.g. a 512x512 interactive
+// frame, C1), where the tiles kernel's single launch has less fixed cost. Measured per step (ms, tiles vs
+// queue): C1 0.13 vs 0.16; 512x512 x1 0.22 vs 0.29; C2 x2 frames (1.8 M) 0.54 vs 0.50; one 1080p frame
+// of C3 (2.1 M) 1.55 vs 1.33.
 uint32_t resolve_schedule(const rt_renderer* r, uint32_t count) {
     if (r->params.schedule) return r->params.schedule;
     const uint64_t samples = (uint64_t)count * r->local_rows() * r->width;
-    return samples < (4ull << 20) ? RT_SCHEDULE_TILES : RT_SCHEDULE_QUEUE;
+    return samples < (3ull << 19) ? RT_SCHEDULE_TILES : RT_SCHEDULE_QUEUE;
 }
 
 // variant 0 = the fastest exact scan measured for the slot count: the culling BVH from 32 slots up, the

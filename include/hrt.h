@@ -63,7 +63,7 @@ typedef struct rt_params {
     uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots, 3 from 9, else 1), 1 simple,
                                   3 packed + deferred exact candidates, 4 conservative culling BVH;
                                   all bit-identical. 2 and 5-10 were removed.    */
-    uint32_t schedule;         /* work schedule of rt_draw / rt_draw_frames: 0 auto (queue from 4M
+    uint32_t schedule;         /* work schedule of rt_draw / rt_draw_frames: 0 auto (queue from 1.5M
                                   samples per draw, else tiles), 1 tiles (one lane per pixel for a
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame

@@ -105,16 +105,16 @@ def test_sample_queue_equals_tiles(case):
 
 
 def test_auto_schedule_by_draw_size():
-    """schedule 0 picks tiles below 4M samples per draw and the sample queue from there on."""
+    """schedule 0 picks tiles below 1.5 Mi samples per draw and the sample queue from there on."""
     sd = scenes.golden_scene("shadow_rendering", 256, 256)
     r = scenes.make_renderer(sd)
-    r.draw_frames(64, 1000, 10)  # 4 Mi samples
+    r.draw_frames(24, 1000, 10)  # 1.5 Mi samples
     assert r.stats().schedule == hrt.RT_SCHEDULE_QUEUE
     r.draw_frames(1, 2000, 10)
     assert r.stats().schedule == hrt.RT_SCHEDULE_TILES
     t = scenes.make_renderer(sd)
     t.set_params(schedule=hrt.RT_SCHEDULE_TILES)
-    t.draw_frames(64, 1000, 10)
+    t.draw_frames(24, 1000, 10)
     t.draw_frames(1, 2000, 10)
     np.testing.assert_array_equal(r.read_image().view(np.uint32), t.read_image().view(np.uint32))
 
