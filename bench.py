@@ -107,6 +107,8 @@ def main() -> int:
     ap.add_argument("--suspend-below", type=int, default=None,
                     help="sample queue, sphere BVH: suspend a wave's walks below this many walking lanes "
                          "(default: the library's)")
+    ap.add_argument("--queue-budget-mb", type=int, default=None,
+                    help="sample queue: colour-buffer budget per chunk in MiB (default: the library's)")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -157,6 +159,8 @@ def main() -> int:
     extra = {} if args.suspend_below is None else {"suspend_below": args.suspend_below}
     if args.job_frames is not None:
         extra["job_frames"] = args.job_frames
+    if args.queue_budget_mb is not None:
+        extra["queue_budget_mb"] = args.queue_budget_mb
     r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
                  schedule=args.schedule, tri_bvh=args.tri_bvh, **extra)
     local_rows = r.local_rows

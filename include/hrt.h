@@ -68,7 +68,7 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 4096   */
+    uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 32768  */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 16       */
     uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
                                   parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
