@@ -319,6 +319,10 @@ def main() -> int:
                 "flop_per_launch": flop_per_launch,
                 "alg_hbm_bytes_per_launch": alg_bytes,
                 "hbm_gbs_alg": round(alg_bytes / (avg_launch_ms * 1e-3) / 1e9, 3),
+                # the north star's HBM view: measured bytes (committed PMC pass) per launch time,
+                # against the ~8 TB/s peak — HBM is not this path's bound
+                "hbm_gbs_traffic": (round(traffic / (avg_launch_ms * 1e-3) / 1e9, 3) if traffic else None),
+                "hbm_frac": (round(traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
             },
         }
         if not args.no_cpu_baseline and world == 1:
