@@ -1248,14 +1248,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
 // (BvhQuery in registers, stack in LDS), as soon as fewer than `suspend_below` lanes of the wave are still
 // walking; the finished lanes shade, start their next query (or sample) and all lanes walk on together.
 // Every lane computes exactly the same query as k_trace, so the sample colours are bit-identical.
-// A 20-entry stack (20 KB of LDS per workgroup; 24 entries would cap the CU at 6 workgroups). 6 waves per
-// SIMD (80-VGPR budget): the frame-block primary rays (7 VGPRs) measured +3.5 % on C3 at 6 waves over the
-// per-lane primary rays at 7 waves (72 VGPRs), which in turn were +1.6 % over 6; with them 7 waves spill.
-constexpr int SPLIT_STACK = 20;
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split(const KParams P) {
+// 7 waves per SIMD (72-VGPR budget; 6 VGPRs spilled): the frame block lives in LDS (8 KB per workgroup)
+// next to a 14-entry stack (14 KB), 22 KB x 7 workgroups fitting the CU's 160 KB. Measured on C3: block in
+// VGPRs at 6 waves (20-entry stack) 26.1 Grays/s, block in LDS at 7 waves 26.5; per-lane primary rays were
+// 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
+constexpr int SPLIT_STACK = 14;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     const uint32_t lane = threadIdx.x & 63u;
     __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
+    __shared__ float4 blk[2 * 256];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
@@ -1272,11 +1274,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     BvhQuery Q;
     // Primary rays are generated a frame-block at a time: when the wave's block (one frame of its job's
     // 8x8 tile) is used up, every lane computes the primary ray of its own pixel for the next frame at
-    // once (all lanes busy), and lanes that need a sample fetch one from the block's owner lane with
-    // cross-lane reads, instead of each freed lane computing its own with a few lanes active.
+    // once (all lanes busy) into the wave's slice of `blk`, and lanes that need a sample read theirs from
+    // it, instead of each freed lane computing its own with a few lanes active.
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
-    f3 pr_o = mk(0.0f, 0.0f, 0.0f), pr_d = mk(0.0f, 0.0f, 0.0f);
-    uint32_t pr_s = 0, pr_ok = 0;  // this lane's pixel's primary ray for the block, and whether it exists
     while (true) {
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
@@ -1301,20 +1301,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 blk_next = 0;
                 const uint32_t x = (job_tile % P.tiles_w) * 8u + (lane & 7u);
                 const uint32_t kr = (job_tile / P.tiles_w) * 8u + (lane >> 3);
-                pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
-                if (pr_ok) {
+                const uint32_t pok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
+                Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
+                uint32_t ps = 0;
+                if (pok) {
                     const uint32_t y = P.row0 + kr * P.row_step;
-                    const Ray pr = primary_ray<MODE>(P, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, pr_s);
-                    pr_o = pr.o;
-                    pr_d = pr.d;
+                    pr = primary_ray<MODE>(P, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, ps);
                 }
+                blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
+                blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const uint32_t avail = 64u - blk_next;
             const uint32_t rank = (uint32_t)__popcll(m & below);
             const int src = (int)((blk_next + rank) & 63u);
-            const float ox = __shfl(pr_o.x, src), oy = __shfl(pr_o.y, src), oz = __shfl(pr_o.z, src);
-            const float dx = __shfl(pr_d.x, src), dy = __shfl(pr_d.y, src), dz = __shfl(pr_d.z, src);
-            const uint32_t ss = __shfl(pr_s, src), ok = __shfl(pr_ok, src);
+            const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src)];
+            const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src) + 1];
+            const float ox = b0.x, oy = b0.y, oz = b0.z, dx = b0.w, dy = b1.x, dz = b1.y;
+            const uint32_t ss = __float_as_uint(b1.z), ok = __float_as_uint(b1.w);
             if (need && rank < avail) {
                 need = false;
                 if (ok) {
