@@ -270,7 +270,8 @@ def main() -> int:
             except Exception:  # noqa: BLE001
                 traffic = None
         out = {
-            "metric": ("Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)" if args.config == "c3"
+            "metric": ("Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)"
+                       if args.config == "c3" and (sd.width, sd.height, sd.frames) == (1920, 1080, 1024)
                        else f"Mrays/sec, {sd.name} {sd.width}x{sd.height}x{sd.frames}spp x {sd.bounces}-bounce"),
             "value": round(value, 2),
             "unit": "Mrays/s",
