@@ -257,7 +257,7 @@ __device__ __forceinline__ bool padded_box_hit_nb(const float4 mn, const float4 
 // bvh_end (winner slot, or the exact full scan for the fallback cases).
 struct BvhQuery {
     Slab S;
-    float a4, a2, bt;
+    float bt;
     int bc;          // running winner as a code: BVH-order position (< nleaf) or nleaf + large-list index
     uint32_t node;   // next child word to visit
     int sp;
@@ -271,11 +271,10 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 // Returns true when the walk has to run (false: bvh_end does the full scan).
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
-    Q.a4 = 4.0f * a;
-    Q.a2 = 2.0f * a;
+    const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
     Q.sp = 0;
     const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
-    if (!(Q.a2 > 0x1p-100f && Q.a2 < 0x1p100f) || !finite_o) {
+    if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
         Q.full_scan = 1u;
 #ifdef HRT_DEBUG_SPLIT
         atomicAdd(P.counter + 5, 1ull);
@@ -290,7 +289,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     int bc = -1;
     for (uint32_t k = 0; k < P.nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
-        const float t = exact_t_geo(P.sph_geo[i], r, Q.a4, Q.a2);
+        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
         if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
     tally.spheres += P.nlarge;
@@ -322,7 +321,8 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                                         Tally& tally, uint32_t below) {
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
-    const float a4 = Q.a4, a2 = Q.a2;
+    const float a = dot(r.d, r.d);  // the same value bvh_begin computed
+    const float a4 = 4.0f * a, a2 = 2.0f * a;
     uint32_t node = Q.node;
     int sp = Q.sp;
     float bt = Q.bt;
@@ -1248,7 +1248,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
 // (BvhQuery in registers, stack in LDS), as soon as fewer than `suspend_below` lanes of the wave are still
 // walking; the finished lanes shade, start their next query (or sample) and all lanes walk on together.
 // Every lane computes exactly the same query as k_trace, so the sample colours are bit-identical.
-// 7 waves per SIMD (72-VGPR budget; 6 VGPRs spilled): the frame block lives in LDS (8 KB per workgroup)
+// 7 waves per SIMD (72-VGPR budget, no spills since bvh_run recomputes a = d.d instead of carrying it): the
+// frame block lives in LDS (8 KB per workgroup)
 // next to a 14-entry stack (14 KB), 22 KB x 7 workgroups fitting the CU's 160 KB. Measured on C3: block in
 // VGPRs at 6 waves (20-entry stack) 26.1 Grays/s, block in LDS at 7 waves 26.5; per-lane primary rays were
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
