@@ -1241,6 +1241,80 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 
     }
 }
 
+// Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
+// compiles spill-free there): when the wave's block (one frame
+// of its job's 8x8 tile) is used up, every lane computes its own pixel's primary ray for the next frame at
+// once into the wave's slice of `blk` (two float4 per lane), and lanes that need a sample read theirs.
+struct BlockState {
+    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+};
+
+template <int MODE>
+__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, float4* blk, bool& drained,
+                                                 uint32_t lane, unsigned long long below, bool& have,
+                                                 uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
+                                                 uint32_t& bounce, uint32_t& pix, uint32_t& fl) {
+    bool need = !have && !drained;
+    unsigned long long m = __ballot(need);
+    while (m != 0ull) {
+        if (B.blk_next == 64u) {
+            if (B.blk_f + 1u < B.job_nf) {
+                B.blk_f++;
+            } else {
+                unsigned long long j = 0;
+                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                j = __shfl(j, 0);
+                if (j >= P.njobs) {
+                    drained = true;
+                    break;
+                }
+                const uint32_t chunk = (uint32_t)(j % P.nchunks);
+                B.job_tile = (uint32_t)(j / P.nchunks);
+                B.job_f0 = chunk * P.job_frames;
+                B.job_nf = min(P.job_frames, P.nframes - B.job_f0);
+                B.blk_f = 0;
+            }
+            B.blk_next = 0;
+            const uint32_t x = (B.job_tile % P.tiles_w) * 8u + (lane & 7u);
+            const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
+            const uint32_t pok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
+            Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
+            uint32_t ps = 0;
+            if (pok) {
+                const uint32_t y = P.row0 + kr * P.row_step;
+                pr = primary_ray<MODE>(P, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, ps);
+            }
+            blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
+            blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const uint32_t avail = 64u - B.blk_next;
+        const uint32_t rank = (uint32_t)__popcll(m & below);
+        const uint32_t src = (B.blk_next + rank) & 63u;
+        const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + src)];
+        const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + src) + 1];
+        if (need && rank < avail) {
+            need = false;
+            if (__float_as_uint(b1.w)) {
+                ray.o = mk(b0.x, b0.y, b0.z);
+                ray.d = mk(b0.w, b1.x, b1.y);
+                s = __float_as_uint(b1.z);
+                fl = B.job_f0 + B.blk_f;
+                pix = B.job_tile * 64u + src;
+                sky_t = ray.d.y * 0.5f + 0.5f;
+                att = mk(1.0f, 1.0f, 1.0f);
+                bounce = 0;
+                have = true;
+                qs = 0;
+            }
+        }
+        B.blk_next += min((uint32_t)__popcll(m), avail);
+        m = __ballot(need);
+    }
+}
+
 // Sample queue with suspendable walks (sphere program, culling BVH; rt_params.suspend_below > 0).
 // In k_trace a wave's query step lasts as long as its slowest lane's walk: secondary rays of one wave
 // take very different paths through the tree, so most lanes idle at the end of every step (PMC of
@@ -1436,7 +1510,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
-    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    __shared__ float4 blk[2 * 256];  // the wave's frame block (refill_block_lds)
+    BlockState B;
     bool drained = false;
     Ray ray;
     f3 att = mk(1.0f, 1.0f, 1.0f);
@@ -1448,47 +1523,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     int bi = -1;  // sphere winner slot
     HeapWalk W;
     while (true) {
-        bool need = !have && !drained;
-        unsigned long long m = __ballot(need);
-        while (m != 0ull) {
-            if (job_next == job_total) {
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(P.queue, 1ull);
-                j = __shfl(j, 0);
-                if (j >= P.njobs) {
-                    drained = true;
-                    break;
-                }
-                const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                job_tile = (uint32_t)(j / P.nchunks);
-                job_f0 = chunk * P.job_frames;
-                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
-                job_next = 0;
-            }
-            const uint32_t avail = job_total - job_next;
-            const uint32_t rank = (uint32_t)__popcll(m & below);
-            if (need && rank < avail) {
-                const uint32_t sid = job_next + rank;
-                const uint32_t l = sid & 63u;
-                fl = job_f0 + (sid >> 6);
-                pix = job_tile * 64u + l;
-                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
-                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
-                need = false;
-                if (x < P.W && kr < P.nrows) {
-                    const uint32_t y = P.row0 + kr * P.row_step;
-                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
-                    sky_t = ray.d.y * 0.5f + 0.5f;
-                    att = mk(1.0f, 1.0f, 1.0f);
-                    bounce = 0;
-                    have = true;
-                    qs = 0;
-                }
-            }
-            const uint32_t took = min((uint32_t)__popcll(m), avail);
-            job_next += took;
-            m = __ballot(need);
-        }
+        refill_block_lds<MODE>(P, B, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
         if (drained && __ballot(have) == 0ull) break;
         if (have && qs == 0u) {
             if (bounce >= P.bounces) {
