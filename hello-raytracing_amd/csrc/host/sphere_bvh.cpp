@@ -51,6 +51,9 @@ struct Builder {
     uint32_t max_leaf = BVH_MAX_LEAF;
     uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
     double traversal_cost = 0.5;
+    // binned SAH over all three axes with 32 bins (HRT_BVH_ALL_AXES=0: the widest axis, 16 bins, as first
+    // built): C3 26.9 -> 27.7 Grays/s, 16.8 -> 16.2 box and 5.4 -> 4.9 sphere tests per ray
+    bool all_axes = true;
 
     uint32_t leaf_word(size_t first, size_t count) {
         uint32_t f = (uint32_t)out->slot.size();
@@ -80,39 +83,48 @@ struct Builder {
         int axis = 0;
         for (int k = 1; k < 3; k++)
             if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
-        const float ext = chi[axis] - clo[axis];
 
         size_t mid = first + count / 2;
-        bool use_median = depth >= 20 || !(ext > 0.0f);
+        bool use_median = depth >= 20 || !(chi[axis] - clo[axis] > 0.0f);
         if (!use_median) {
-            constexpr int NB = 16;
-            Box bb[NB];
-            size_t bc[NB] = {0};
-            auto bin_of = [&](const Prim& p) {
-                int i = (int)((p.cen[axis] - clo[axis]) / ext * NB);
-                return std::min(NB - 1, std::max(0, i));
-            };
-            for (size_t i = first; i < first + count; i++) {
-                int k = bin_of(prims[i]);
-                bb[k].grow(prims[i].box);
-                bc[k]++;
-            }
+            constexpr int NB = 32;
             double best = std::numeric_limits<double>::infinity();
-            int best_k = -1;
-            for (int k = 1; k < NB; k++) {
-                Box L, R;
-                size_t nl = 0, nr = 0;
-                for (int j = 0; j < k; j++) { if (bc[j]) { L.grow(bb[j]); nl += bc[j]; } }
-                for (int j = k; j < NB; j++) { if (bc[j]) { R.grow(bb[j]); nr += bc[j]; } }
-                if (!nl || !nr) continue;
-                double cost = L.area() * (double)nl + R.area() * (double)nr;
-                if (cost < best) { best = cost; best_k = k; }
+            int best_k = -1, best_axis = axis;
+            // binned SAH over every axis with extent (all_axes) or the widest one
+            for (int ax = 0; ax < 3; ax++) {
+                if (!all_axes && ax != axis) continue;
+                const float ext = chi[ax] - clo[ax];
+                if (!(ext > 0.0f)) continue;
+                Box bb[NB];
+                size_t bc[NB] = {0};
+                for (size_t i = first; i < first + count; i++) {
+                    int k = (int)((prims[i].cen[ax] - clo[ax]) / ext * (all_axes ? NB : 16));
+                    k = std::min((all_axes ? NB : 16) - 1, std::max(0, k));
+                    bb[k].grow(prims[i].box);
+                    bc[k]++;
+                }
+                const int nb = all_axes ? NB : 16;
+                for (int k = 1; k < nb; k++) {
+                    Box L, R;
+                    size_t nl = 0, nr = 0;
+                    for (int j = 0; j < k; j++) { if (bc[j]) { L.grow(bb[j]); nl += bc[j]; } }
+                    for (int j = k; j < nb; j++) { if (bc[j]) { R.grow(bb[j]); nr += bc[j]; } }
+                    if (!nl || !nr) continue;
+                    double cost = L.area() * (double)nl + R.area() * (double)nr;
+                    if (cost < best) { best = cost; best_k = k; best_axis = ax; }
+                }
             }
             const double leaf_cost = b.area() * (double)count;
             if (count <= max_leaf && !(best + traversal_cost * b.area() < leaf_cost)) return leaf_word(first, count);
             if (best_k < 0) {
                 use_median = true;
             } else {
+                const int ax = best_axis, nb = all_axes ? NB : 16;
+                const float ext = chi[ax] - clo[ax];
+                auto bin_of = [&](const Prim& p) {
+                    int i = (int)((p.cen[ax] - clo[ax]) / ext * nb);
+                    return std::min(nb - 1, std::max(0, i));
+                };
                 auto it = std::stable_partition(prims.begin() + (long)first, prims.begin() + (long)(first + count),
                                                 [&](const Prim& p) { return bin_of(p) < best_k; });
                 mid = (size_t)(it - prims.begin());
@@ -161,6 +173,7 @@ SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
     if (const char* e = std::getenv("HRT_BVH_MAX_LEAF")) b.max_leaf = std::max(1, std::min(15, std::atoi(e)));
     if (const char* e = std::getenv("HRT_BVH_LEAF_DEPTH")) b.leaf_depth = (uint32_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("HRT_BVH_TRAVERSAL_COST")) b.traversal_cost = std::atof(e);
+    if (const char* e = std::getenv("HRT_BVH_ALL_AXES")) b.all_axes = std::atoi(e) != 0;
     bool any = false;
     for (size_t i = 0; i < n; i++) {
         const float* s = &cr[4 * i];
