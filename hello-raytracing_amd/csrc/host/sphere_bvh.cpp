@@ -51,9 +51,12 @@ struct Builder {
     uint32_t max_leaf = BVH_MAX_LEAF;
     uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
     double traversal_cost = 0.5;
-    // binned SAH over all three axes with 32 bins (HRT_BVH_ALL_AXES=0: the widest axis, 16 bins, as first
-    // built): C3 26.9 -> 27.7 Grays/s, 16.8 -> 16.2 box and 5.4 -> 4.9 sphere tests per ray
+    // binned SAH over all three axes (HRT_BVH_ALL_AXES=0: the widest axis, 16 bins, as first built). C3,
+    // Grays/s by bin count: 8 25.9, 16 26.8, 24 26.9, 32 27.7, 48 26.8, 64 28.0 (box / sphere tests per ray
+    // 16.0 / 4.5 at 64, 16.8 / 5.4 first); an exact sweep SAH gave 26.9: tree shape matters more than
+    // SAH accuracy here, and 64 bins measured best
     bool all_axes = true;
+    int bins = 64;  // HRT_BVH_BINS (2..64) with all_axes
 
     uint32_t leaf_word(size_t first, size_t count) {
         uint32_t f = (uint32_t)out->slot.size();
@@ -87,7 +90,7 @@ struct Builder {
         size_t mid = first + count / 2;
         bool use_median = depth >= 20 || !(chi[axis] - clo[axis] > 0.0f);
         if (!use_median) {
-            constexpr int NB = 32;
+            const int NB = bins;
             double best = std::numeric_limits<double>::infinity();
             int best_k = -1, best_axis = axis;
             // binned SAH over every axis with extent (all_axes) or the widest one
@@ -95,8 +98,8 @@ struct Builder {
                 if (!all_axes && ax != axis) continue;
                 const float ext = chi[ax] - clo[ax];
                 if (!(ext > 0.0f)) continue;
-                Box bb[NB];
-                size_t bc[NB] = {0};
+                Box bb[64];
+                size_t bc[64] = {0};
                 for (size_t i = first; i < first + count; i++) {
                     int k = (int)((prims[i].cen[ax] - clo[ax]) / ext * (all_axes ? NB : 16));
                     k = std::min((all_axes ? NB : 16) - 1, std::max(0, k));
@@ -174,6 +177,7 @@ SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
     if (const char* e = std::getenv("HRT_BVH_LEAF_DEPTH")) b.leaf_depth = (uint32_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("HRT_BVH_TRAVERSAL_COST")) b.traversal_cost = std::atof(e);
     if (const char* e = std::getenv("HRT_BVH_ALL_AXES")) b.all_axes = std::atoi(e) != 0;
+    if (const char* e = std::getenv("HRT_BVH_BINS")) b.bins = std::max(2, std::min(64, std::atoi(e)));
     bool any = false;
     for (size_t i = 0; i < n; i++) {
         const float* s = &cr[4 * i];
