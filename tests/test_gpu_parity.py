@@ -170,45 +170,53 @@ def test_row_partition_matches_full_image():
         np.testing.assert_array_equal(r.read_image().view(np.uint32), fimg[row0::step].view(np.uint32))
 
 
-def test_resume_from_checkpoint_is_bitwise():
+@pytest.mark.parametrize("schedule", [0, 2])
+def test_resume_from_checkpoint_is_bitwise(schedule):
     sd = scenes.golden_scene("metal_materials", 64, 64)
     r = scenes.make_renderer(sd)
+    r.set_params(schedule=schedule)
     r.draw_frames(8, 1000, 10)
     want = r.read_image()
     a = scenes.make_renderer(sd)
+    a.set_params(schedule=schedule)
     a.draw_frames(3, 1000, 10)
     ck, fc = a.read_image(), a.frame_count
     b = scenes.make_renderer(sd)
+    b.set_params(schedule=schedule)
     b.write_image(ck)
     b.set_frame_count(fc)
     b.draw_frames(5, 1030, 10)
     np.testing.assert_array_equal(b.read_image().view(np.uint32), want.view(np.uint32))
 
 
-def test_ema_cap_and_bounce_params():
+@pytest.mark.parametrize("schedule", [0, 2])
+def test_ema_cap_and_bounce_params(schedule):
     sd = scenes.golden_scene("shadow_rendering", 48, 40)
     r = scenes.make_renderer(sd)
-    r.set_params(ema_cap=3, bounces=2)
+    r.set_params(ema_cap=3, bounces=2, schedule=schedule)
     r.draw_frames(7, 500, 7)
     ref, q = scenes.oracle_render(sd, frames=7, time0=500, dtime=7, ema_cap=3, bounces=2)
     assert_parity(r.read_image(), ref, "ema_cap=3 bounces=2")
     assert r.stats().queries == q
 
 
-def test_zero_bounces_is_sky_only():
+@pytest.mark.parametrize("schedule", [0, 2])
+def test_zero_bounces_is_sky_only(schedule):
     sd = scenes.golden_scene("lambertian_materials", 32, 32)
     r = scenes.make_renderer(sd)
-    r.set_params(bounces=0)
+    r.set_params(bounces=0, schedule=schedule)
     r.draw_frames(2, 1000, 10)
     ref, q = scenes.oracle_render(sd, frames=2, bounces=0)
     assert q == 0 and r.stats().queries == 0
     assert_parity(r.read_image(), ref, "bounces=0")
 
 
-def test_empty_sphere_scene_and_reset():
+@pytest.mark.parametrize("schedule", [0, 2])
+def test_empty_sphere_scene_and_reset(schedule):
     sd = scenes.golden_scene("lambertian_materials", 40, 30)
     sd.spheres = hrt.spheres_array([])
     r = scenes.make_renderer(sd)
+    r.set_params(schedule=schedule)
     r.draw_frames(3, 1000, 10)
     ref, _ = scenes.oracle_render(sd, frames=3)
     assert_parity(r.read_image(), ref, "empty scene (100 zero slots)")
