@@ -49,7 +49,7 @@ struct Prim {
 };
 
 constexpr uint32_t MAX_LEAF = 4;
-constexpr int BINS = 16;
+constexpr int BINS = 32;  // over 3 axes (C4 with the SAH walk: 16 bins 16.3, 32 17.0, 64 17.0 Grays/s)
 
 struct Builder {
     std::vector<Prim> prims;
@@ -77,44 +77,46 @@ struct Builder {
         int axis = 0;
         for (int k = 1; k < 3; k++)
             if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
-        const double ext = chi[axis] - clo[axis];
         size_t mid = first + count / 2;
-        bool median = depth >= 48 || !(ext > 0.0);
+        bool median = depth >= 48 || !(chi[axis] - clo[axis] > 0.0);
         if (!median) {
-            Box bb[BINS];
-            size_t bc[BINS] = {0};
-            auto bin_of = [&](const Prim& p) {
-                const int i = (int)((p.cen[axis] - clo[axis]) / ext * BINS);
-                return std::min(BINS - 1, std::max(0, i));
-            };
-            for (size_t i = first; i < first + count; i++) {
-                const int k = bin_of(prims[i]);
-                bb[k].grow(prims[i].box);
-                bc[k]++;
-            }
-            // sweep: right-side boxes from the top, then the left side incrementally
-            Box rb[BINS];
-            size_t rc[BINS] = {0};
-            Box acc;
-            size_t nacc = 0;
-            for (int k = BINS - 1; k >= 1; k--) {
-                acc.grow(bb[k]);
-                nacc += bc[k];
-                rb[k] = acc;
-                rc[k] = nacc;
-            }
+            // binned SAH over every axis with extent (the sphere BVH's builder found 3 axes better than the
+            // widest one: host/sphere_bvh.cpp)
             double best = std::numeric_limits<double>::infinity();
-            int best_k = -1;
-            Box lacc;
-            size_t nl = 0;
-            for (int k = 1; k < BINS; k++) {
-                lacc.grow(bb[k - 1]);
-                nl += bc[k - 1];
-                if (!nl || !rc[k]) continue;
-                const double cost = lacc.area() * (double)nl + rb[k].area() * (double)rc[k];
-                if (cost < best) {
-                    best = cost;
-                    best_k = k;
+            int best_k = -1, best_axis = axis;
+            for (int ax = 0; ax < 3; ax++) {
+                const double ex = chi[ax] - clo[ax];
+                if (!(ex > 0.0)) continue;
+                Box bb[BINS];
+                size_t bc[BINS] = {0};
+                for (size_t i = first; i < first + count; i++) {
+                    const int k = std::min(BINS - 1, std::max(0, (int)((prims[i].cen[ax] - clo[ax]) / ex * BINS)));
+                    bb[k].grow(prims[i].box);
+                    bc[k]++;
+                }
+                // sweep: right-side boxes from the top, then the left side incrementally
+                Box rb[BINS];
+                size_t rc[BINS] = {0};
+                Box acc;
+                size_t nacc = 0;
+                for (int k = BINS - 1; k >= 1; k--) {
+                    acc.grow(bb[k]);
+                    nacc += bc[k];
+                    rb[k] = acc;
+                    rc[k] = nacc;
+                }
+                Box lacc;
+                size_t nl = 0;
+                for (int k = 1; k < BINS; k++) {
+                    lacc.grow(bb[k - 1]);
+                    nl += bc[k - 1];
+                    if (!nl || !rc[k]) continue;
+                    const double cost = lacc.area() * (double)nl + rb[k].area() * (double)rc[k];
+                    if (cost < best) {
+                        best = cost;
+                        best_k = k;
+                        best_axis = ax;
+                    }
                 }
             }
             // leaf when splitting does not pay (1 = relative cost of a box test vs a triangle test)
@@ -122,6 +124,12 @@ struct Builder {
             if (best_k < 0) {
                 median = true;
             } else {
+                const int ax = best_axis;
+                const double ex = chi[ax] - clo[ax];
+                auto bin_of = [&](const Prim& p) {
+                    const int i = (int)((p.cen[ax] - clo[ax]) / ex * BINS);
+                    return std::min(BINS - 1, std::max(0, i));
+                };
                 auto it = std::partition(prims.begin() + (long)first, prims.begin() + (long)(first + count),
                                          [&](const Prim& p) { return bin_of(p) < best_k; });
                 mid = (size_t)(it - prims.begin());
