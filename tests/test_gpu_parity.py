@@ -65,6 +65,19 @@ def test_golden_scene_hip_vs_oracle_and_golden(name):
     assert stats.samples == 512 * 512  # last draw() = one frame
 
 
+@pytest.mark.parametrize("name", scenes.GOLDEN_NAMES)
+def test_golden_scene_full_draw_sample_queue(name):
+    """The same golden scenes at full size drawn as one 100-frame draw: the sample queue with the
+    suspendable-walk kernel (100 slots -> culling BVH) equals the per-frame reference protocol bit for bit."""
+    sd = scenes.golden_scene(name)
+    per_frame = render_reference_protocol(sd, scenes.GOLDEN_FRAMES).renderer.read_image()
+    r = scenes.make_renderer(sd)
+    r.draw_frames(scenes.GOLDEN_FRAMES, 1000, 10)
+    st = r.stats()
+    assert st.schedule == hrt.RT_SCHEDULE_QUEUE and st.suspend_below > 0 and st.variant == 4
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), per_frame.view(np.uint32))
+
+
 def test_draw_frames_equals_per_frame_draws():
     sd = scenes.golden_scene("complex_scene", 96, 64)
     a = render_reference_protocol(sd, 12).renderer.read_image()
