@@ -471,7 +471,10 @@ int rt_device_count(void) {
     return n;
 }
 
-const char* rt_build_info(void) { return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_render<sphere|tris|mixed>"; }
+const char* rt_build_info(void) {
+    return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_trace_split, k_trace_split_tris, k_trace, k_accumulate, "
+           "k_render";
+}
 
 int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     if (!out || width == 0 || height == 0) return fail(RT_ERR_ARG, "rt_create: null out or zero size");
