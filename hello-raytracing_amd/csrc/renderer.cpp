@@ -389,8 +389,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
             // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the
             // heap walk of the triangle / mixed programs with a linear sphere scan; not the opt-in SAH walk
-            const bool split = !P.tri_bvh && (r->mode == RT_MODE_SPHERE ? variant == hrt_dev::SCAN_BVH
-                                                                         : variant != hrt_dev::SCAN_BVH);
+            const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
             P.suspend_below = split ? r->params.suspend_below : 0u;
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;

@@ -424,10 +424,11 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
+template <int STACK = BVH_STACK>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin(P, r, best, Q, tally)) bvh_run<false>(P, r, Q, stack, tally, 0u);
+    if (bvh_begin(P, r, best, Q, tally)) bvh_run<false, STACK>(P, r, Q, stack, tally, 0u);
     return bvh_end(P, r, Q, best, tally);
 }
 
@@ -1487,18 +1488,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 }
 
 // Sample queue with suspendable walks for the triangle and mixed programs (reference heap walk; the
-// sphere part of the mixed program is the linear scan `SCAN`, simple or deferred). A lane's query goes
-// begin (sphere scan) -> heap walk -> shade; the wave suspends the walks once fewer than
-// `suspend_below` lanes are still walking, so lanes whose rays miss the mesh (one node test) do not idle
-// behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s). Bit-identical to k_trace, with the same
-// node/triangle counts. (The mixed program with the culling BVH stays on k_trace: a two-phase split,
-// sphere walk then heap walk, measured slower on C5.)
+// sphere part of the mixed program is `SCAN`: the linear scan, simple or deferred, or the culling BVH
+// walked to completion). A lane's query goes begin (sphere scan) -> heap walk -> shade; the wave
+// suspends the heap walk once fewer than `suspend_below` lanes are still walking, so lanes whose rays
+// miss the mesh (one node test) do not idle behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s;
+// C5: 6.25 -> 6.55). Bit-identical to k_trace, with the same node/triangle counts.
 template <int MODE, int SCAN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
-    static_assert(SCAN != SCAN_BVH, "the mixed program with the culling BVH runs k_trace");
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t tri_list[TRI_BATCH * 256];  // per-lane deferred-triangle list
+    // per-lane deferred-triangle list; with the culling BVH also the sphere walk's stack (never live together:
+    // the sphere scan finishes in the begin phase)
+    __shared__ uint32_t tri_list[TRI_BATCH * 256];
     uint32_t* const cand = tri_list + threadIdx.x;
     uint16_t* defer_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
@@ -1534,9 +1535,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 qs = 3u;
             } else {
                 float sb = FLT_MAX_REF;
-                if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<(int)TRI_BATCH>(P, ray, sb, cand, tally);
+                else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
-                tally.spheres += P.nslots;
+                if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
                 heap_begin(ray, sb, W);
                 qs = 3u;
             }
@@ -1638,14 +1640,16 @@ template <int MODE, bool TSAH>
 static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t stream) {
     if constexpr (MODE != MODE_SPHERE && !TSAH) {
         if (P.suspend_below > 0u) {
-            // (the host sets suspend_below = 0 for the mixed program with the culling BVH: a two-phase split,
-            // sphere walk then heap walk, measured slower than k_trace on C5 at 256 spp — 6.10 Grays/s
-            // unsplit, 5.93 with both phases split at 16, 6.05 with the heap walk split only)
+            // The mixed program with the culling BVH runs its sphere walk to completion in the begin phase
+            // (stack in the triangle-batch LDS) and suspends only the heap walk: C5 at 256 spp 6.25 -> 6.55
+            // Grays/s. (Splitting both walks measured 5.93; an earlier heap-only form with the stack in
+            // the LDS block region, 6.05.)
             if constexpr (MODE == MODE_TRIS) {
                 return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
             } else {
                 if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
                 if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream);
+                return launch_persistent(k_trace_split_tris<MODE, SCAN_BVH>, P, stream);
             }
         }
     }

@@ -299,8 +299,8 @@ def test_suspendable_walks_bit_identical(suspend_below):
 def test_suspendable_heap_walk_bit_identical(variant):
     """k_trace_split_tris (mixed program: sphere scan `variant`, then the reference heap walk, suspendable)
     gives the oracle's bits and ray counts, and k_trace's node/triangle test counts (the walk itself is
-    unchanged); the triangle program on Suzanne and the dragon likewise. Variant 4 (culling BVH) keeps
-    k_trace whatever suspend_below says."""
+    unchanged); the triangle program on Suzanne and the dragon likewise. With variant 4 (culling BVH) the
+    sphere walk finishes in the begin phase and only the heap walk suspends."""
     sd = scenes.config_c4(96, 72, 4)
     if variant == 4:
         sd.spheres = np.concatenate([sd.spheres] + [scenes.rtiow_spheres()[:60]])  # >= 32 slots: culling BVH
@@ -317,7 +317,8 @@ def test_suspendable_heap_walk_bit_identical(variant):
             r.set_params(variant=v if sd.mode != hrt.RT_MODE_TRIS else 0, schedule=2, suspend_below=sb)
             r.draw_frames(sd.frames, 1000, 10)
             st = r.stats()
-            counts.append((st.queries, st.node_tests, st.tri_tests))
+            assert st.suspend_below == sb
+            counts.append((st.queries, st.node_tests, st.tri_tests, st.sphere_tests))
             img = r.read_image()
             if sb == 16:
                 ref, q = scenes.oracle_render(sd)
