@@ -450,6 +450,34 @@ def test_culling_bvh_with_zero_radius_slots():
         np.testing.assert_array_equal(out[0].view(np.uint32), img.view(np.uint32))
 
 
+def test_split_walk_stack_overflow_falls_back_to_the_exact_scan():
+    """2^17 coincident spheres: the culling BVH degenerates to 15 levels of median splits with every box
+    hit, so k_trace_split's 14-entry LDS stack overflows and those queries fall back to the exact full
+    scan (more sphere tests than k_trace with its 24-entry stack). Every t ties, so the lowest slot must
+    win: slot 0 is the only lambertian among eight materials tiled over the slots. Both kernels give the
+    oracle's bits."""
+    base = [hrt.Sphere.new_lambertian(hrt.Vec3(0.0, 0.0, -3.0), 1.0, hrt.Vec3(0.9, 0.3, 0.2))]
+    base += [hrt.Sphere.new_metal(hrt.Vec3(0.0, 0.0, -3.0), 1.0, hrt.Vec3(0.1 * k, 0.8, 0.5), 0.05 * k)
+             for k in range(1, 8)]
+    sph = np.tile(hrt.spheres_array(base), 1 << 14)
+    cam = hrt.Camera.new(hrt.Vec3(0.0, 0.5, 1.0), hrt.Vec3(0.0, 0.0, -3.0), 4.0, 0.0, 0.9)
+    sd = scenes.SceneDef("coincident", hrt.RT_MODE_SPHERE, 24, 16, cam, sph, frames=2, bounces=8,
+                         min_sphere_slots=0)
+    runs = {}
+    for sb in (0, 24):
+        r = scenes.make_renderer(sd)
+        r.set_params(variant=4, schedule=hrt.RT_SCHEDULE_QUEUE, suspend_below=sb)
+        r.draw_frames(sd.frames, 1000, 10)
+        runs[sb] = (r.read_image(), r.stats())
+    (img0, st0), (img1, st1) = runs[0], runs[24]
+    assert st0.suspend_below == 0 and st1.suspend_below == 24 and st1.queries == st0.queries
+    assert st1.sphere_tests > st0.sphere_tests, (st1.sphere_tests, st0.sphere_tests)  # the fallback ran
+    np.testing.assert_array_equal(img0.view(np.uint32), img1.view(np.uint32))
+    ref, q = scenes.oracle_render(sd)
+    assert q == st1.queries
+    assert_parity(img1, ref, "coincident spheres, stack overflow")
+
+
 def test_suzanne_tris_mode_vs_oracle():
     scene = hrt.SceneTris.new_suzane(128, 96)
     scene.init()
