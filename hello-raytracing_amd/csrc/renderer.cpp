@@ -386,10 +386,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.nframes = std::min(chunk, count - done);
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
-            P.job_frames = std::max<uint32_t>(1u, r->params.job_frames);
             // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the
-            // heap walk of the triangle / mixed programs with a linear sphere scan; not the opt-in SAH walk
+            // heap walk of the triangle / mixed programs; not the opt-in SAH walk
             const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
+            // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for
+            // k_trace's cheap sphere scans (C2: 32 costs 3 %)
+            P.job_frames = r->params.job_frames ? r->params.job_frames : (split ? 32u : 16u);
             P.suspend_below = split ? r->params.suspend_below : 0u;
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
@@ -500,7 +502,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.queue_budget_mb = 32768;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
-    r->params.job_frames = 16;
+    r->params.job_frames = 0;  // per kernel (rt_draw_frames)
     // measured: C3 (sphere) 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s (first split
     //           kernel); with the frame-block refill and 16-frame jobs 16 -> 25.2, 24 -> 25.9, 32 -> 25.2;
     //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92

@@ -69,7 +69,8 @@ typedef struct rt_params {
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 32768  */
-    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 16       */
+    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 0 = per
+                                  kernel: 32 with the suspendable walks, 16 for the linear sphere scans */
     uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
                                   parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
                                   same closest hit except where the reference's 600-step cap or

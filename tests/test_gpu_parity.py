@@ -651,3 +651,4 @@ def test_bad_arguments_fail_loudly():
             r.set_params(**bad)           # a suspend threshold above the wave width
     assert hrt.Renderer(8, 8, hrt.RT_MODE_SPHERE).params.suspend_below == 24  # per-program defaults
     assert r.params.suspend_below == 32
+    assert r.params.job_frames == 0  # per kernel: 32 with the suspendable walks, 16 for the linear scans
