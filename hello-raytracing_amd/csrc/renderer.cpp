@@ -105,6 +105,7 @@ struct rt_renderer {
     uint32_t n_spheres = 0;
     // culling BVH over the sphere slots (SCAN_BVH)
     DevBuf<float4> bvh_nodes, bvh_sph;
+    DevBuf<uint4> bvh_hnodes;
     DevBuf<int> bvh_slot, bvh_large;
     hrt::SphereBvh bvh_host;
     DevBuf<float4> nodes;
@@ -160,6 +161,44 @@ std::vector<float4> pack_bvh_nodes(const std::vector<hrt::SphereBvhNode>& nodes,
         o[1] = float4{rel_hi(n.lmax[0], 0), rel_hi(n.lmax[1], 1), rel_hi(n.lmax[2], 2), 0.0f};
         o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
         o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
+    }
+    return out;
+}
+
+// The culling BVH's nodes with fp16 boxes (k_trace_split): 32 B per node instead of 64 — per child the
+// box relative to `center` as six halves rounded outward (min down, max up: containment holds, so the walk
+// stays exact; the boxes only grow by at most one half ulp), then the child word:
+//   (min.x | min.y << 16, min.z | max.x << 16, max.y | max.z << 16, left word), the same for the right.
+uint16_t f16_bits(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
+_Float16 f16_from_bits(uint16_t b) { return __builtin_bit_cast(_Float16, b); }
+_Float16 f16_step(_Float16 h, bool up) {
+    uint16_t b = f16_bits(h);
+    if ((b & 0x7FFFu) == 0u) return f16_from_bits(up ? 0x0001u : 0x8001u);  // +-0 -> smallest subnormal
+    const bool neg = (b & 0x8000u) != 0u;
+    b = (uint16_t)((up != neg) ? b + 1u : b - 1u);
+    return f16_from_bits(b);
+}
+uint32_t f16_dir(float x, bool up) {
+    _Float16 h = (_Float16)x;
+    if (up ? (float)h < x : (float)h > x) h = f16_step(h, up);
+    return f16_bits(h);
+}
+std::vector<uint4> pack_bvh_hnodes(const std::vector<hrt::SphereBvhNode>& nodes, const float center[3]) {
+    std::vector<uint4> out(2 * std::max<size_t>(nodes.size(), 1), uint4{0u, 0u, 0u, 0u});
+    auto rel = [&](float v, int k, bool up) {
+        const float f = std::nextafter((float)((double)v - (double)center[k]), up ? INFINITY : -INFINITY);
+        return f16_dir(f, up);
+    };
+    for (size_t j = 0; j < nodes.size(); j++) {
+        const hrt::SphereBvhNode& n = nodes[j];
+        const float* mn[2] = {n.lmin, n.rmin};
+        const float* mx[2] = {n.lmax, n.rmax};
+        const uint32_t w[2] = {n.left, n.right};
+        for (int c = 0; c < 2; c++) {
+            out[2 * j + c] = uint4{rel(mn[c][0], 0, false) | rel(mn[c][1], 1, false) << 16,
+                                   rel(mn[c][2], 2, false) | rel(mx[c][0], 0, true) << 16,
+                                   rel(mx[c][1], 1, true) | rel(mx[c][2], 2, true) << 16, w[c]};
+        }
     }
     return out;
 }
@@ -220,11 +259,13 @@ int upload_spheres(rt_renderer* r) {
     r->bvh_host = hrt::build_sphere_bvh(cr);
     const hrt::SphereBvh& B = r->bvh_host;
     const std::vector<float4> bnodes = pack_bvh_nodes(B.nodes, B.root_center);
+    const std::vector<uint4> hnodes = pack_bvh_hnodes(B.nodes, B.root_center);
     const size_t nleaf = B.slot.size();
     int rc = ensure(r->sph_geo, nslots);
     if (!rc) rc = ensure(r->sph_aux, nslots);
     if (!rc) rc = ensure(r->sph_pairs, npairs);
     if (!rc) rc = ensure(r->bvh_nodes, bnodes.size());
+    if (!rc) rc = ensure(r->bvh_hnodes, hnodes.size());
     if (!rc) rc = ensure(r->bvh_sph, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_slot, std::max<size_t>(nleaf, 1));
     if (!rc) rc = ensure(r->bvh_large, std::max<size_t>(B.large.size(), 1));
@@ -235,6 +276,8 @@ int upload_spheres(rt_renderer* r) {
         HIP_TRY(hipMemcpyAsync(r->sph_pairs.ptr, pairs.data(), npairs * sizeof(pairs[0]), hipMemcpyHostToDevice,
                                r->stream));
         HIP_TRY(hipMemcpyAsync(r->bvh_nodes.ptr, bnodes.data(), bnodes.size() * sizeof(float4),
+                               hipMemcpyHostToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->bvh_hnodes.ptr, hnodes.data(), hnodes.size() * sizeof(uint4),
                                hipMemcpyHostToDevice, r->stream));
         if (nleaf) {
             HIP_TRY(hipMemcpyAsync(r->bvh_sph.ptr, B.sph.data(), nleaf * sizeof(float4), hipMemcpyHostToDevice,
@@ -355,6 +398,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.bvh_root = B.root_word;
     for (int k = 0; k < 3; k++) P.bvh_rc[k] = B.root_center[k];
     P.bvh_rr = B.root_radius;
+    P.bvh_hnodes = r->bvh_hnodes.ptr;
+    // fp16 boxes reach up to one half ulp (2^-11 relative) past the f32 root box
+    P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;

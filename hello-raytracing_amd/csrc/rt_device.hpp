@@ -89,6 +89,8 @@ struct KParams {
     uint32_t nlarge, bvh_root;    // large-list length, root child word
     uint32_t bvh_nleaf, pad_l;    // spheres in the BVH (bvh_sph / bvh_slot entries)
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
+    const uint4* bvh_hnodes;      // the nodes with fp16 boxes, 2 uint4 per node (k_trace_split; renderer.cpp)
+    float bvh_rr_h, pad_h16;      // radius bound of the fp16 boxes; unused
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp): 4 float4 per node like bvh_nodes
     const float4* tb_nodes;

@@ -269,6 +269,7 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 }
 
 // Returns true when the walk has to run (false: bvh_end does the full scan).
+template <bool H16 = false>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -299,7 +300,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     // per-query padding: delta >= the distance by which a float-accepted sphere can miss geometrically
     const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
     const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
-    const float D = dl * 1.001f + P.bvh_rr;
+    const float D = dl * 1.001f + (H16 ? P.bvh_rr_h : P.bvh_rr);
     const float dn = __builtin_amdgcn_sqrtf(a);
     const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
     const float pad = 2.02f * delta;
@@ -316,7 +317,13 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
 
 // The walk. Returns true when it has finished; with SUSPEND it may return false after a pop, once fewer
 // than `below` lanes of the wave are still walking (every call makes progress: the check follows a pop).
-template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false>
+typedef _Float16 hrt_h2 __attribute__((ext_vector_type(2)));
+// fp16 box decode for the k_trace_split walk (P.bvh_hnodes): the slab FMAs take the halves directly
+// (v_fma_mix_f32: the f16 operand is widened exactly inside the f32 FMA, no conversions).
+__device__ __forceinline__ float h16_lo(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).x; }
+__device__ __forceinline__ float h16_hi(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).y; }
+
+template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below) {
     const float4* __restrict__ nodes = P.bvh_nodes;
@@ -338,10 +345,19 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 if (first_active_lane()) tally.wbox++;
             }
 #endif
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
+            float4 n0, n1, n2, n3;
+            if constexpr (H16) {
+                const uint4 c0 = P.bvh_hnodes[2 * node], c1 = P.bvh_hnodes[2 * node + 1];
+                n0 = float4{h16_lo(c0.x), h16_hi(c0.x), h16_lo(c0.y), __uint_as_float(c0.w)};
+                n1 = float4{h16_hi(c0.y), h16_lo(c0.z), h16_hi(c0.z), 0.0f};
+                n2 = float4{h16_lo(c1.x), h16_hi(c1.x), h16_lo(c1.y), __uint_as_float(c1.w)};
+                n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
+            } else {
+                n0 = nodes[4 * node + 0];
+                n1 = nodes[4 * node + 1];
+                n2 = nodes[4 * node + 2];
+                n3 = nodes[4 * node + 3];
+            }
             float tl, tr;
             // SELECT (k_trace_split): best-t bound as a separate compare (no per-step canonicalize of bt)
             // and select-form child order, +1 % on C3; the three-way branch below keeps k_trace's mixed
@@ -424,11 +440,11 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
-template <int STACK = BVH_STACK>
+template <int STACK = BVH_STACK, bool H16 = true>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin(P, r, best, Q, tally)) bvh_run<false, STACK>(P, r, Q, stack, tally, 0u);
+    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16>(P, r, Q, stack, tally, 0u);
     return bvh_end(P, r, Q, best, tally);
 }
 
@@ -1421,13 +1437,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #endif
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
-                qs = bvh_begin(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+                qs = bvh_begin<true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
             } else {  // bounce cap 0: the sample is the sky colour
                 qs = 3u;
             }
         }
         if (have && qs == 1u) {
-            if (bvh_run<true, SPLIT_STACK, true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
+            if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
         }
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
