@@ -119,7 +119,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
-    ap.add_argument("--cpu-frames", type=int, default=64)
+    ap.add_argument("--cpu-frames", type=int, default=128)
     args = ap.parse_args()
 
     import numpy as np

@@ -1096,7 +1096,9 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // (shader_sphere.wgsl:264-271), so the image is bit-identical to k_render's and to count x rt_draw.
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TSAH ? 5 : 6))) void k_trace(const KParams P) {
+// (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    TSAH || (MODE == MODE_MIXED && SCAN == SCAN_DEFER) ? 5 : 6))) void k_trace(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     const LaneLists lists = lane_lists<MODE, SCAN>();
     void* const lds_list = lists.sphere;
@@ -1510,7 +1512,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // miss the mesh (one node test) do not idle behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s;
 // C5: 6.25 -> 6.55). Bit-identical to k_trace, with the same node/triangle counts.
 template <int MODE, int SCAN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_split_tris(const KParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
+k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
     const uint32_t lane = threadIdx.x & 63u;
     // per-lane deferred-triangle list; with the culling BVH also the sphere walk's stack (never live together:
