@@ -116,7 +116,7 @@ struct rt_renderer {
     std::vector<float> tri_aee;  // a, e1, e2 of every triangle as uploaded
     bool tri_tree_dirty = true;
     hrt::TriBvh tri_tree;
-    DevBuf<float4> tb_nodes;
+    DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
     DevBuf<float> samples;  // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major
@@ -206,11 +206,11 @@ std::vector<uint4> pack_bvh_hnodes(const std::vector<hrt::SphereBvhNode>& nodes,
 int upload_tri_tree(rt_renderer* r) {
     if (!r->tri_tree_dirty) return RT_OK;
     r->tri_tree = hrt::build_tri_bvh(r->tri_aee);
-    const std::vector<float4> packed = pack_bvh_nodes(r->tri_tree.nodes, r->tri_tree.root_center);
-    int rc = ensure(r->tb_nodes, packed.size());
+    const std::vector<uint4> hpacked = pack_bvh_hnodes(r->tri_tree.nodes, r->tri_tree.root_center);
+    int rc = ensure(r->tb_hnodes, hpacked.size());
     if (!rc) rc = ensure(r->tb_order, std::max<size_t>(r->tri_tree.order.size(), 1));
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(r->tb_nodes.ptr, packed.data(), packed.size() * sizeof(float4), hipMemcpyHostToDevice,
+    HIP_TRY(hipMemcpyAsync(r->tb_hnodes.ptr, hpacked.data(), hpacked.size() * sizeof(uint4), hipMemcpyHostToDevice,
                            r->stream));
     if (!r->tri_tree.order.empty())
         HIP_TRY(hipMemcpyAsync(r->tb_order.ptr, r->tri_tree.order.data(), r->tri_tree.order.size() * sizeof(uint32_t),
@@ -370,7 +370,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     if (P.tri_bvh) {
         rc = upload_tri_tree(r);
         if (rc) return rc;
-        P.tb_nodes = r->tb_nodes.ptr;
+        P.tb_hnodes = r->tb_hnodes.ptr;
+        P.tb_rr_h = std::nextafter(r->tri_tree.root_radius * (1.0f + 0x1p-9f), INFINITY);
         P.tb_order = r->tb_order.ptr;
         P.tb_root = r->tri_tree.root_word;
         for (int k = 0; k < 3; k++) P.tb_rc[k] = r->tri_tree.root_center[k];

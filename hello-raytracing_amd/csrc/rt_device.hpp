@@ -89,14 +89,16 @@ struct KParams {
     uint32_t nlarge, bvh_root;    // large-list length, root child word
     uint32_t bvh_nleaf, pad_l;    // spheres in the BVH (bvh_sph / bvh_slot entries)
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
-    const uint4* bvh_hnodes;      // the nodes with fp16 boxes, 2 uint4 per node (k_trace_split; renderer.cpp)
-    float bvh_rr_h, pad_h16;      // radius bound of the fp16 boxes; unused
+    const uint4* bvh_hnodes;      // the nodes with fp16 boxes, 2 uint4 per node (every sphere-BVH walk;
+                                  // renderer.cpp pack_bvh_hnodes); bvh_nodes is the f32 form (bvh_run<.., false>)
+    float bvh_rr_h, pad_h16;      // radius bound of the fp16 boxes (>= their half-diagonal); padding
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
-    // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp): 4 float4 per node like bvh_nodes
-    const float4* tb_nodes;
+    // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp), nodes with fp16 boxes like bvh_hnodes
     const uint32_t* tb_order;     // triangle index of each leaf entry
     uint32_t tb_root, tri_bvh;    // root child word; 1 = walk the SAH tree instead of the reference heap
     float tb_rc[3], tb_rr;        // root box centre (nodes are relative to it) and radius bound
+    const uint4* tb_hnodes;       // 2 uint4 per node (renderer.cpp pack_bvh_hnodes)
+    float tb_rr_h, tb_pad16;      // radius bound of the fp16 boxes; padding
     const float4* nodes;          // 2 float4 per node: min, max
     const TriDev* tris;
     const MatDev* mats;

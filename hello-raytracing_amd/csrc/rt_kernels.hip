@@ -322,6 +322,15 @@ typedef _Float16 hrt_h2 __attribute__((ext_vector_type(2)));
 // (v_fma_mix_f32: the f16 operand is widened exactly inside the f32 FMA, no conversions).
 __device__ __forceinline__ float h16_lo(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).x; }
 __device__ __forceinline__ float h16_hi(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).y; }
+// a node with fp16 boxes (2 uint4) as the 4 float4 of the f32 layout: lmin|left, lmax, rmin|right, rmax
+__device__ __forceinline__ void load_hnode(const uint4* __restrict__ hn, uint32_t node, float4& n0, float4& n1,
+                                           float4& n2, float4& n3) {
+    const uint4 c0 = hn[2 * node], c1 = hn[2 * node + 1];
+    n0 = float4{h16_lo(c0.x), h16_hi(c0.x), h16_lo(c0.y), __uint_as_float(c0.w)};
+    n1 = float4{h16_hi(c0.y), h16_lo(c0.z), h16_hi(c0.z), 0.0f};
+    n2 = float4{h16_lo(c1.x), h16_hi(c1.x), h16_lo(c1.y), __uint_as_float(c1.w)};
+    n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
+}
 
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
@@ -347,11 +356,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #endif
             float4 n0, n1, n2, n3;
             if constexpr (H16) {
-                const uint4 c0 = P.bvh_hnodes[2 * node], c1 = P.bvh_hnodes[2 * node + 1];
-                n0 = float4{h16_lo(c0.x), h16_hi(c0.x), h16_lo(c0.y), __uint_as_float(c0.w)};
-                n1 = float4{h16_hi(c0.y), h16_lo(c0.z), h16_hi(c0.z), 0.0f};
-                n2 = float4{h16_lo(c1.x), h16_hi(c1.x), h16_lo(c1.y), __uint_as_float(c1.w)};
-                n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
+                load_hnode(P.bvh_hnodes, node, n0, n1, n2, n3);
             } else {
                 n0 = nodes[4 * node + 0];
                 n1 = nodes[4 * node + 1];
@@ -640,7 +645,7 @@ constexpr int TRI_STACK = 24;
 __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
                                          uint32_t* stack) {
     const f3 op = mk(r.o.x - P.tb_rc[0], r.o.y - P.tb_rc[1], r.o.z - P.tb_rc[2]);
-    const float D = __builtin_amdgcn_sqrtf(dot(op, op)) * 1.001f + P.tb_rr;
+    const float D = __builtin_amdgcn_sqrtf(dot(op, op)) * 1.001f + P.tb_rr_h;
     const float pad = D * 0x1p-12f;
     Slab S;
     S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
@@ -650,16 +655,13 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
     S.lo = S.lo * S.inv;
     S.hi = S.hi * S.inv;
 #endif
-    const float4* __restrict__ nodes = P.tb_nodes;
     uint32_t node = P.tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
     int sp = 0;
     uint32_t overflow = 0u;  // an integer, not an i1 lane mask (see bvh_run)
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
+            float4 n0, n1, n2, n3;
+            load_hnode(P.tb_hnodes, node, n0, n1, n2, n3);
             float tl, tr;
             const bool hl = padded_box_hit(n0, n1, S, best, tl);
             const bool hr = padded_box_hit(n2, n3, S, best, tr);
