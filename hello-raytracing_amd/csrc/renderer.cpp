@@ -139,6 +139,10 @@ struct rt_renderer {
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
 };
 
+#ifndef HRT_LNODES
+#define HRT_LNODES 1
+#endif
+
 namespace {
 
 int zero_image(rt_renderer* r) {
@@ -402,6 +406,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.bvh_hnodes = r->bvh_hnodes.ptr;
     // fp16 boxes reach up to one half ulp (2^-11 relative) past the f32 root box
     P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
+    P.bvh_nnodes = (uint32_t)B.nodes.size();
+    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= 192u && B.depth <= 8u) ? 1u : 0u;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;

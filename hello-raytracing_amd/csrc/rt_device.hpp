@@ -91,7 +91,9 @@ struct KParams {
     float bvh_rc[3], bvh_rr;      // root box centre and radius bound
     const uint4* bvh_hnodes;      // the nodes with fp16 boxes, 2 uint4 per node (every sphere-BVH walk;
                                   // renderer.cpp pack_bvh_hnodes); bvh_nodes is the f32 form (bvh_run<.., false>)
-    float bvh_rr_h, pad_h16;      // radius bound of the fp16 boxes (>= their half-diagonal); padding
+    float bvh_rr_h;               // radius bound of the fp16 boxes (>= their half-diagonal)
+    uint32_t bvh_nnodes;          // nodes in bvh_hnodes
+    uint32_t bvh_lnodes, pad_ln;  // 1: k_trace_split keeps the nodes in LDS (<= 192 nodes, depth <= 8)
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp), nodes with fp16 boxes like bvh_hnodes
     const uint32_t* tb_order;     // triangle index of each leaf entry

@@ -334,7 +334,7 @@ __device__ __forceinline__ void load_hnode(const uint4* __restrict__ hn, uint32_
 
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
-                                        Tally& tally, uint32_t below) {
+                                        Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
     const float a = dot(r.d, r.d);  // the same value bvh_begin computed
@@ -356,7 +356,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #endif
             float4 n0, n1, n2, n3;
             if constexpr (H16) {
-                load_hnode(P.bvh_hnodes, node, n0, n1, n2, n3);
+                load_hnode(hn, node, n0, n1, n2, n3);
             } else {
                 n0 = nodes[4 * node + 0];
                 n1 = nodes[4 * node + 1];
@@ -449,7 +449,7 @@ template <int STACK = BVH_STACK, bool H16 = true>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16>(P, r, Q, stack, tally, 0u);
+    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
     return bvh_end(P, r, Q, best, tally);
 }
 
@@ -1348,11 +1348,20 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // next to a 14-entry stack (14 KB), 22 KB x 7 workgroups fitting the CU's 160 KB. Measured on C3: block in
 // VGPRs at 6 waves (20-entry stack) 26.1 Grays/s, block in LDS at 7 waves 26.5; per-lane primary rays were
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
-constexpr int SPLIT_STACK = 14;
+// LNODES (small trees: <= LNODE_CAP nodes, depth <= 8): the fp16 nodes are copied into LDS once per
+// workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
+constexpr int LNODE_CAP = 192;
+template <bool LNODES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
+    constexpr int SPLIT_STACK = LNODES ? 8 : 14;
     const uint32_t lane = threadIdx.x & 63u;
     __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
+    __shared__ uint4 lnodes[LNODES ? 2 * LNODE_CAP : 1];
+    if constexpr (LNODES) {
+        for (uint32_t i = threadIdx.x; i < 2u * P.bvh_nnodes; i += 256u) lnodes[i] = P.bvh_hnodes[i];
+        __syncthreads();
+    }
     __shared__ float4 blk[2 * 256];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
@@ -1447,7 +1456,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             }
         }
         if (have && qs == 1u) {
-            if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below)) qs = 2u;
+            if constexpr (LNODES) {
+                if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
+            } else {
+                if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
+                    qs = 2u;
+            }
         }
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
@@ -1687,7 +1701,9 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     if (P.njobs == 0) return hipSuccess;
     switch (mode) {
     case MODE_SPHERE:
-        if (variant == SCAN_BVH && P.suspend_below > 0u) return launch_persistent(k_trace_split, P, stream);
+        if (variant == SCAN_BVH && P.suspend_below > 0u)
+            return P.bvh_lnodes ? launch_persistent(k_trace_split<true>, P, stream)
+                                : launch_persistent(k_trace_split<false>, P, stream);
         return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
     case MODE_TRIS:
         return P.tri_bvh ? launch_trace_mode<MODE_TRIS, true>(variant, P, stream)
