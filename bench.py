@@ -68,6 +68,93 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: the box's CPU share (16 per GPU on the pool), at most the visible CPUs."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_info() -> dict:
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        import psutil
+
+        physical = psutil.cpu_count(logical=False)
+    except Exception:  # noqa: BLE001
+        physical = None
+    return {"cpu_model": model, "physical_cores_visible": physical, "logical_cpus_visible": os.cpu_count()}
+
+
+def find_pmc(config: str, width: int, height: int, spp: int, world: int, kernel: str):
+    """The committed PMC summary (scripts/pmc.sh -> profiles/rNN/*pmc_summary.json) of exactly this workload:
+    same config, resolution, spp, one rank, and the same kernel symbol. None when there is no such pass."""
+    key = {"config": config, "width": width, "height": height, "spp": spp, "ranks": world, "kernel": kernel}
+    for f in sorted((ROOT / "profiles").glob("r*/*pmc_summary.json"), reverse=True):
+        try:
+            pm = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if pm.get("_key") == key:
+            pm["_file"] = str(f.relative_to(ROOT))
+            return pm
+    return None
+
+
+def pmc_view(pm):
+    """Utilisation of the VALU from the PMC pass: issue busy (VALU instructions x 2 cycles per wave64
+    instruction over 1024 SIMDs x the kernel's GPU cycles) and active lanes per issued VALU instruction."""
+    if not pm:
+        return None
+    try:
+        cycles = pm["GRBM_GUI_ACTIVE"] / 8.0  # GRBM counts are summed over the 8 XCDs
+        busy = pm["SQ_INSTS_VALU"] * 2.0 / (1024.0 * cycles)
+        lanes = pm["SQ_THREAD_CYCLES_VALU"] / pm["SQ_ACTIVE_INST_VALU"]
+    except (KeyError, ZeroDivisionError):
+        return {"file": pm.get("_file")}
+    return {"file": pm.get("_file"), "valu_issue_busy": round(busy, 4), "active_lanes": round(lanes, 2),
+            "valu_lane_util": round(busy * lanes / 64.0, 4),
+            "wait_frac": round(pm.get("SQ_WAIT_ANY", 0.0) / max(pm.get("SQ_WAVE_CYCLES", 1.0), 1.0), 4),
+            "salu_insts": pm.get("SQ_INSTS_SALU"), "valu_insts": pm.get("SQ_INSTS_VALU")}
+
+
+def launcher_selftest(args) -> int:
+    """CPU rehearsal of the multi-rank path without a GPU: the self-launched ranks join a gloo group, each fills
+    its interleaved rows of a W x H x 3 image with their global row index, and hrt.parallel.gather_image
+    assembles them on rank 0 — the code path of the real bench minus the renderer."""
+    import torch
+    import torch.distributed as dist
+
+    from hrt.parallel import gather_image, rows_of
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    H, W = 37, 5
+    n = rows_of(rank, world, H)
+    part = torch.zeros((-(-H // world), W, 3), dtype=torch.float32)
+    part[:n] = torch.arange(rank, H, world, dtype=torch.float32)[:, None, None]
+    full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0)
+    if rank == 0:
+        ok = bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32)))
+        print(json.dumps({"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}",
+                          "verify_gather_bitwise": ok}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def cpu_baseline(sd, threads: int, rows: int, frames: int):
     """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload."""
     import scenes
@@ -83,6 +170,10 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "algorithm": (f"linear-scan oracle: every ray tests all {len(sd.spheres)} sphere slots (the reference's "
+                      "algorithm); the GPU kernel culls with a BVH, so the ratio mixes algorithm and hardware"),
+        "threads": threads,
+        **cpu_info(),
         "sample": f"{sd.name}: {n} rows (every {step}th) x {sd.width} px x {frames} frames, {q} rays in {dt:.1f} s",
     }
 
@@ -120,7 +211,18 @@ def main() -> int:
     ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=128)
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU-only rehearsal of the multi-rank path (self-launch, gloo, row-tile gather): no GPU")
     args = ap.parse_args()
+
+    from hrt.launch import needs_self_launch, spawn_ranks
+
+    if needs_self_launch(args.gpus):
+        # no external launcher: run this script as N ranks (torch.distributed.run) before any GPU call here
+        log(f"--gpus {args.gpus} without WORLD_SIZE: launching {args.gpus} ranks on 127.0.0.1")
+        return spawn_ranks(args.gpus, str(Path(__file__).resolve()), sys.argv[1:])
+    if args.launcher_selftest:
+        return launcher_selftest(args)
 
     import numpy as np
     import torch
@@ -180,6 +282,10 @@ def main() -> int:
         r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
         st = r.stats()
         gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full)
+        if world > 1:
+            # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
+            # renderer's own stream, which does not order against it: finish the gather first
+            torch.cuda.current_stream().synchronize()
         return st
 
     log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
@@ -204,8 +310,10 @@ def main() -> int:
     suspend = 0
     trace_ms = 0.0
     trace_launches = 0
+    st_last = None
     for i in range(args.steps):
         st = step()
+        st_last = st
         queries += st.queries
         kernel_ms += st.kernel_ms
         launches += st.launches
@@ -252,23 +360,18 @@ def main() -> int:
         tri_flop = NODE_TEST_FLOP * my_nodes + TRI_TEST_FLOP * my_tris
         flop_per_launch = ((SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP) * my_q + tri_flop) / nl
         achieved = flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
-        executed = ((SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q + tri_flop)
-                    / nl / (avg_launch_ms * 1e-3) / 1e12)
+        executed_flop_per_launch = (SPHERE_TEST_FLOP * my_sph + BOX_TEST_FLOP * my_box + RAY_OVERHEAD_FLOP * my_q
+                                    + tri_flop) / nl
+        executed = executed_flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
         px = local_rows * sd.width
         if schedule == 2:  # k_trace writes one 12 B colour per sample; the sphere arrays are read once
             alg_bytes = 12.0 * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
         else:  # k_render reads and writes the framebuffer once per launch
             alg_bytes = 24.0 * px + 64.0 * nslots
-        traffic = None
-        pmc = ROOT / "profiles" / "pmc_summary.json"
-        if pmc.exists():
-            try:  # the committed PMC pass (scripts/pmc.sh) of this same configuration and kernel
-                pm = json.loads(pmc.read_text())
-                kname = "k_trace" if schedule == 2 else "k_render"
-                if pm.get("_bench_config") == args.config and any(kname in k for k in pm.get("_kernels", [])):
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:  # noqa: BLE001
-                traffic = None
+        kernel_sym = st_last.kernel.decode() if st_last is not None else ""
+        pmc = find_pmc(args.config, sd.width, sd.height, sd.frames, world, kernel_sym)
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        executed_tflops = executed
         out = {
             "metric": ("Mrays/sec at 1920x1080x1024spp x 50-bounce (RTIOW cover scene)"
                        if args.config == "c3" and (sd.width, sd.height, sd.frames) == (1920, 1080, 1024)
@@ -286,6 +389,7 @@ def main() -> int:
             "data": "synthetic (seeded RTIOW-style scene, committed generator tests/scenes.py)",
             "config": {
                 "workload": sd.name,
+                "id": args.config,
                 "width": sd.width,
                 "height": sd.height,
                 "spp": sd.frames,
@@ -295,40 +399,46 @@ def main() -> int:
                 "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
                 "parallelism": f"rows{world}",
             },
+            # The path is FP32-VALU issue bound (no MFMA: no dense contraction; HBM ~2 % busy). `achieved` =
+            # the FP32 FLOPs the kernel executes (its exact in-kernel test counters x FLOP per test, + the
+            # per-ray hit record / scatter) / the HIP-event time of its launches on the renderer's stream.
             "roofline": {
                 "bound": "fp32-valu",
-                "achieved": round(achieved, 3),
+                "achieved": round(executed_tflops, 3),
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "frac": round(executed_tflops / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": (f"k_render<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if schedule != 2
-                           else f"k_trace<{MODE_NAMES[sd.mode]}, scan variant {variant}>" if not suspend
-                           else f"k_trace_split (sphere, culling BVH, suspend below {suspend} lanes)"
-                           if sd.mode == 0 else
-                           f"k_trace_split_tris<{MODE_NAMES[sd.mode]}, scan variant {variant}> (suspend below {suspend})"),
+                "kernel": kernel_sym,
                 "schedule": {1: "tiles", 2: "sample-queue"}.get(schedule, str(schedule)),
+                "suspend_below": suspend,
+                "sphere_variant": variant,
+                "avg_launch_ms": round(avg_launch_ms, 3),
+                "launches_per_step": round(nl / args.steps, 3),
                 "all_kernels_ms_per_step": round(float(all_t[0, 8]) / args.steps, 3),
+                "flop_model": {"sphere_test": SPHERE_TEST_FLOP, "box_test": BOX_TEST_FLOP, "per_ray": RAY_OVERHEAD_FLOP,
+                               "heap_node_test": NODE_TEST_FLOP, "tri_test": TRI_TEST_FLOP},
                 "sphere_tests_per_ray": round(my_sph / max(my_q, 1.0), 3),
                 "box_tests_per_ray": round(my_box / max(my_q, 1.0), 3),
                 "tri_node_tests_per_ray": round(my_nodes / max(my_q, 1.0), 3),
                 "tri_tests_per_ray": round(my_tris / max(my_q, 1.0), 3),
-                "executed_tflops": round(executed, 3),
-                "executed_frac": round(executed / FP32_PEAK_TFLOPS, 4),
-                "algorithmic_flop_per_ray": SPHERE_TEST_FLOP * nslots + RAY_OVERHEAD_FLOP,
-                "avg_launch_ms": round(avg_launch_ms, 3),
-                "flop_per_launch": flop_per_launch,
+                "executed_flop_per_launch": executed_flop_per_launch,
+                # SURVEY 8(d)'s per-ray price of the reference algorithm (a linear scan over every slot): the
+                # culling BVH delivers that work ~24x faster than it could be executed literally, so this
+                # ratio exceeds 1 and is not a utilisation
+                "linear_scan_equiv_tflops": round(achieved, 3),
+                "linear_scan_equiv_frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "alg_hbm_bytes_per_launch": alg_bytes,
                 "hbm_gbs_alg": round(alg_bytes / (avg_launch_ms * 1e-3) / 1e9, 3),
-                # the north star's HBM view: measured bytes (committed PMC pass) per launch time,
-                # against the ~8 TB/s peak — HBM is not this path's bound
+                # HBM view (north star): the committed PMC pass of this exact config and kernel, per launch
                 "hbm_gbs_traffic": (round(traffic / (avg_launch_ms * 1e-3) / 1e9, 3) if traffic else None),
                 "hbm_frac": (round(traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
+                "pmc": pmc_view(pmc),
             },
         }
         if not args.no_cpu_baseline and world == 1:
             log("cpu baseline (oracle) ...")
-            out["cpu_baseline"] = cpu_baseline(sd, min(16, os.cpu_count() or 1), args.cpu_rows, args.cpu_frames)
+            out["cpu_baseline"] = cpu_baseline(sd, cpu_threads(), args.cpu_rows, args.cpu_frames)
         if not args.no_golden:
             out["golden"] = golden_check()
             log(f"golden: {out['golden']['harness_pass']}/{out['golden']['scenes']} pass the reference harness, "

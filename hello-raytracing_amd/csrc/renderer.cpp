@@ -23,6 +23,7 @@
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
+const char* hrt_last_kernel();
 
 namespace {
 
@@ -477,6 +478,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.samples = (uint64_t)count * P.nrows * r->width;
     r->stats.launches = launches;
     r->stats.local_rows = P.nrows;
+    std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
     r->timing_pending = true;
     return RT_OK;
 }

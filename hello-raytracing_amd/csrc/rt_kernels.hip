@@ -1650,8 +1650,19 @@ __global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
     px[2] = acc2;
 }
 
+// Demangled-symbol form of the kernel a draw ran ("k_trace_split<true>"): rt_stats.kernel, and the key
+// bench.py matches against rocprofv3 summaries.
+static char g_kernel_name[64] = "";
+const char* hrt_last_kernel() { return g_kernel_name; }
+static const char* kname(const char* base, int a, int b = -1, int c = -1) {
+    if (b < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s>", base, a ? "true" : "false");
+    else if (c < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d>", base, a, b);
+    else snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d, %s>", base, a, b, c ? "true" : "false");
+    return g_kernel_name;
+}
+
 template <typename K>
-static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stream) {
+static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stream, const char* /*name*/) {
     static int cus = 0;
     if (cus == 0) {
         int dev = 0;
@@ -1680,20 +1691,20 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
             // Grays/s. (Splitting both walks measured 5.93; an earlier heap-only form with the stack in
             // the LDS block region, 6.05.)
             if constexpr (MODE == MODE_TRIS) {
-                return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
+                return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream, kname("k_trace_split_tris", MODE, SCAN_SIMPLE));
             } else {
-                if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream);
-                if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream);
-                return launch_persistent(k_trace_split_tris<MODE, SCAN_BVH>, P, stream);
+                if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream, kname("k_trace_split_tris", MODE, SCAN_SIMPLE));
+                if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream, kname("k_trace_split_tris", MODE, SCAN_DEFER));
+                return launch_persistent(k_trace_split_tris<MODE, SCAN_BVH>, P, stream, kname("k_trace_split_tris", MODE, SCAN_BVH));
             }
         }
     }
     if constexpr (MODE == MODE_TRIS) {
-        return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream);
+        return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
     } else {
-        if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream);
-        if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream);
-        return launch_persistent(k_trace<MODE, SCAN_BVH, TSAH>, P, stream);
+        if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
+        if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream, kname("k_trace", MODE, SCAN_DEFER, (int)TSAH));
+        return launch_persistent(k_trace<MODE, SCAN_BVH, TSAH>, P, stream, kname("k_trace", MODE, SCAN_BVH, (int)TSAH));
     }
 }
 
@@ -1702,8 +1713,8 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_BVH && P.suspend_below > 0u)
-            return P.bvh_lnodes ? launch_persistent(k_trace_split<true>, P, stream)
-                                : launch_persistent(k_trace_split<false>, P, stream);
+            return P.bvh_lnodes ? launch_persistent(k_trace_split<true>, P, stream, kname("k_trace_split", 1))
+                                : launch_persistent(k_trace_split<false>, P, stream, kname("k_trace_split", 0));
         return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
     case MODE_TRIS:
         return P.tri_bvh ? launch_trace_mode<MODE_TRIS, true>(variant, P, stream)
@@ -1726,6 +1737,7 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 // variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host).
 template <int MODE, bool TSAH>
 static void launch_render_mode(int variant, const KParams& P, dim3 grid, dim3 block, hipStream_t stream) {
+    (void)kname("k_render", MODE, MODE == MODE_TRIS ? SCAN_SIMPLE : variant, (int)TSAH);
     if constexpr (MODE == MODE_TRIS) {
         hipLaunchKernelGGL((k_render<MODE, SCAN_SIMPLE, TSAH>), grid, block, 0, stream, P);
     } else {

@@ -6,7 +6,7 @@ package is the host-side mirror of the reference's Rust scene API plus ctypes pl
 from ._lib import (LIB_PATH, RT_MODE_MIXED, RT_SCHEDULE_AUTO, RT_SCHEDULE_QUEUE, RT_SCHEDULE_TILES, RT_MODE_SPHERE, RT_MODE_TRIS, RtError, RtParams, RtStats,
                    lib)
 from .scene import (CAMERA_DTYPE, DIELECTRIC, LAMBERTIAN, MATERIAL_DTYPE, MAX_OBJECT_IN_SCENE, METAL,
-                    NODE_DTYPE, PI, SPHERE_DTYPE, TRIANGLE_DTYPE, Camera, ComparisonError, Material, Mesh,
+                    NODE_DTYPE, PI, SPHERE_DTYPE, TRIANGLE_DTYPE, Camera, ComparisonError, Material, Mesh, OrbitCamera,
                     Renderer, SceneSphere, SceneTris, Sphere, Tree, Vec3, compare_ppm_images, f32,
                     ppm_from_image, read_asset, render_ppm, spheres_array)
 
@@ -19,7 +19,7 @@ def device_count() -> int:
 __all__ = [
     "LIB_PATH", "RT_MODE_MIXED", "RT_SCHEDULE_AUTO", "RT_SCHEDULE_QUEUE", "RT_SCHEDULE_TILES", "RT_MODE_SPHERE", "RT_MODE_TRIS", "RtError", "RtParams", "RtStats", "lib",
     "CAMERA_DTYPE", "DIELECTRIC", "LAMBERTIAN", "MATERIAL_DTYPE", "MAX_OBJECT_IN_SCENE", "METAL", "NODE_DTYPE",
-    "PI", "SPHERE_DTYPE", "TRIANGLE_DTYPE", "Camera", "ComparisonError", "Material", "Mesh", "Renderer",
+    "PI", "SPHERE_DTYPE", "TRIANGLE_DTYPE", "Camera", "ComparisonError", "Material", "Mesh", "OrbitCamera", "Renderer",
     "SceneSphere", "SceneTris", "Sphere", "Tree", "Vec3", "compare_ppm_images", "f32", "ppm_from_image",
     "read_asset", "render_ppm", "spheres_array", "device_count",
 ]

@@ -61,6 +61,7 @@ class RtStats(C.Structure):
         ("trace_ms", C.c_double),
         ("trace_launches", C.c_uint32),
         ("suspend_below", C.c_uint32),
+        ("kernel", C.c_char * 64),
     ]
 
 

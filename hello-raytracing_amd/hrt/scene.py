@@ -73,6 +73,58 @@ class Camera:
         return np.frombuffer(out.raw, dtype=CAMERA_DTYPE)[0].copy()
 
 
+def _glam_normalize(v: np.ndarray) -> np.ndarray:
+    """glam 0.24 Vec3::normalize: v * (1 / sqrt(x*x + y*y + z*z)), f32, no FMA."""
+    d = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]
+    return v * (np.float32(1.0) / np.sqrt(d))
+
+
+def _glam_cross(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    return np.array([a[1] * b[2] - b[1] * a[2], a[2] * b[0] - b[2] * a[0], a[0] * b[1] - b[0] * a[1]],
+                    dtype=np.float32)
+
+
+class OrbitCamera:
+    """src/camera_controller.rs:5-129 — the interactive app's camera. Only `to_uniform` crosses the boundary:
+    App re-uploads it every redraw through Scene::update_camera -> Renderer::update_camera_uniform
+    (app.rs:138, mod.rs:52,93, renderer.rs:330-334), the same 80-byte binding as Camera but with w = 0 basis
+    vectors, focal length 10 and no blur — the kernels' 4-component make_ray normalise then acts in 3-D."""
+
+    def __init__(self, aspect_ratio: float, radius: float = 5.0, theta: float = 0.0, phi: float = math.pi / 4.0):
+        self.target = np.zeros(3, dtype=np.float32)
+        self.up = np.array([0.0, 1.0, 0.0], dtype=np.float32)
+        self.fov = f32(math.radians(45.0))  # 45.0_f32.to_radians()
+        self.aspect_ratio = f32(aspect_ratio)
+        self.radius, self.theta, self.phi = f32(radius), f32(theta), f32(phi)
+        self.update_position()
+
+    def update_position(self) -> None:
+        """camera_controller.rs:60-71 (f32 sin/cos; the host libm's, not pinned against Rust's)."""
+        self.phi = f32(min(max(self.phi, f32(0.1)), f32(math.pi) - f32(0.1)))
+        sp, cp = np.sin(self.phi, dtype=np.float32), np.cos(self.phi, dtype=np.float32)
+        st, ct = np.sin(self.theta, dtype=np.float32), np.cos(self.theta, dtype=np.float32)
+        x, y, z = self.radius * sp * ct, self.radius * cp, self.radius * sp * st
+        self.position = self.target + np.array([x, y, z], dtype=np.float32)
+
+    def build_view_matrix(self):
+        """camera_controller.rs:107-113: forward, up, right."""
+        forward = _glam_normalize(self.target - self.position)
+        right = _glam_normalize(_glam_cross(forward, self.up))
+        up = _glam_normalize(_glam_cross(right, forward))
+        return forward, up, right
+
+    def to_uniform(self) -> np.ndarray:
+        """camera_controller.rs:116-129: CameraUniform {eye.w = 1, direction/up/right .w = 0, 10, 0, fov, 0}."""
+        forward, up, right = self.build_view_matrix()
+        u = np.zeros((), dtype=CAMERA_DTYPE)
+        u["eye"] = np.append(self.position, np.float32(1.0))
+        u["direction"] = np.append(forward, np.float32(0.0))
+        u["up"] = np.append(up, np.float32(0.0))
+        u["right"] = np.append(right, np.float32(0.0))
+        u["params"] = np.array([10.0, 0.0, self.fov, 0.0], dtype=np.float32)
+        return u
+
+
 class Material:
     """src/scene/material.rs:17-37."""
 

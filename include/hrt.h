@@ -104,6 +104,8 @@ typedef struct rt_stats {
     uint32_t trace_launches; /* launches of those kernels (the dominant kernel's launch count)          */
     uint32_t suspend_below; /* walks suspended below this many walking lanes in the last draw (k_trace_split*);
                               0 = every query ran to completion (k_trace, k_render)                    */
+    char kernel[64];       /* the ray-tracing kernel the last draw ran, as rocprofv3 names it without
+                              "void " and the argument list, e.g. "k_trace_split<true>"                 */
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

@@ -15,4 +15,4 @@ for grp in \
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$out" -o "p$i" -- python3 bench.py --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1
 done
-python3 scripts/pmc_summary.py "$out" "${PMC_KERNEL:-k_trace}"
+python3 scripts/pmc_summary.py "$out" ${PMC_KERNEL:-}

@@ -42,17 +42,24 @@ def _header_struct(name):
     text = (ROOT / "include" / "hrt.h").read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), text, flags=re.S).group(1)
-    return [(t, n.strip()) for t, names in re.findall(r"(uint32_t|uint64_t|double)\s+([\w\s,]+);", body)
+    return [(t, n.strip()) for t, names in re.findall(r"(uint32_t|uint64_t|double|char)\s+([\w\s,\[\]]+);", body)
             for n in names.split(",")]
 
 
 def test_struct_layouts_match_header():
     ctypes_of = {"uint32_t": C.c_uint32, "uint64_t": C.c_uint64, "double": C.c_double}
+
+    def ctype(t, f):
+        m = re.fullmatch(r"(\w+)\[(\d+)\]", f)
+        return (m.group(1), {"char": C.c_char}[t] * int(m.group(2))) if m else (f, ctypes_of[t])
+
     for py, name in ((hrt.RtParams, "rt_params"), (hrt.RtStats, "rt_stats")):
-        fields = _header_struct(name)
-        assert [(f, ctypes_of[t]) for t, f in fields] == list(py._fields_), name
+        fields = [ctype(t, f) for t, f in _header_struct(name)]
+        got = [(f, t) for f, t in py._fields_]
+        assert [f for f, _ in fields] == [f for f, _ in got], name
+        assert [C.sizeof(t) for _, t in fields] == [C.sizeof(t) for _, t in got], name
     assert C.sizeof(hrt.RtParams) == 12 * 4
-    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4
+    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
 

@@ -78,6 +78,27 @@ def test_golden_scene_full_draw_sample_queue(name):
     np.testing.assert_array_equal(r.read_image().view(np.uint32), per_frame.view(np.uint32))
 
 
+@pytest.mark.parametrize("schedule", [1, 2])
+def test_orbit_camera_uniform_vs_oracle(schedule):
+    """The interactive app's camera path: OrbitCamera::to_uniform (camera_controller.rs:116-129, w = 0 basis,
+    focal 10, blur 0) uploaded through rt_set_camera as Renderer::update_camera_uniform does
+    (renderer.rs:330-334): the 4-component make_ray normalise acts in 3-D and the image matches the oracle."""
+    sd = scenes.golden_scene("complex_scene", 96, 64)
+    cam = hrt.OrbitCamera(sd.width / sd.height, radius=7.0, theta=0.9, phi=1.2)
+    cam.target = np.array([0.0, 0.0, -5.0], dtype=np.float32)
+    cam.update_position()
+    sd.camera = cam.to_uniform()
+    assert float(sd.camera["direction"][3]) == 0.0 and float(sd.camera["params"][0]) == 10.0
+    sd.frames = 6
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=schedule)
+    r.draw_frames(sd.frames, 1000, 10)
+    img = r.read_image()
+    ref, q = scenes.oracle_render(sd)
+    assert_parity(img, ref, f"orbit camera, schedule {schedule}")
+    assert r.stats().queries == q
+
+
 def test_draw_frames_equals_per_frame_draws():
     sd = scenes.golden_scene("complex_scene", 96, 64)
     a = render_reference_protocol(sd, 12).renderer.read_image()
