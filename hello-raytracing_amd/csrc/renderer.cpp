@@ -339,20 +339,24 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, RT_RAW_COUNTERS * sizeof(unsigned long long), r->stream));
 
     hrt_dev::KParams P{};
-    const hrt::Camera& c = r->camera;
-    const float* cam = &c.eye.x;
-    for (int i = 0; i < 4; i++) {
-        P.eye[i] = cam[i];
-        P.dir[i] = cam[4 + i];
-        P.up[i] = cam[8 + i];
-        P.right[i] = cam[12 + i];
+    {
+        hrt_dev::CamDev& cd = P.cam;
+        const hrt::Camera& c = r->camera;
+        const float* cam = &c.eye.x;
+        for (int i = 0; i < 4; i++) {
+            cd.eye[i] = cam[i];
+            cd.dir[i] = cam[4 + i];
+            cd.up[i] = cam[8 + i];
+            cd.right[i] = cam[12 + i];
+        }
+        cd.focal = c.params.x;
+        cd.blur = c.params.y;
+        cd.k = std::tan(c.params.z * 0.5f);  // tan(camera.fov*0.5), make_ray :124 (libm tanf, as the oracle)
+        cd.aspect = (float)r->width / (float)r->height;
+        cd.wm1 = (float)r->width - 1.0f;
+        cd.hm1 = (float)r->height - 1.0f;
+        cd.H = r->height;
     }
-    P.focal = c.params.x;
-    P.blur = c.params.y;
-    P.k = std::tan(c.params.z * 0.5f);  // tan(camera.fov*0.5), make_ray :124 (libm tanf, as the oracle)
-    P.aspect = (float)r->width / (float)r->height;
-    P.wm1 = (float)r->width - 1.0f;
-    P.hm1 = (float)r->height - 1.0f;
     P.W = r->width;
     P.H = r->height;
     P.dtime = dtime;
@@ -408,7 +412,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     // fp16 boxes reach up to one half ulp (2^-11 relative) past the f32 root box
     P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
     P.bvh_nnodes = (uint32_t)B.nodes.size();
-    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= 192u && B.depth <= 8u) ? 1u : 0u;
+    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH) ? 1u : 0u;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;

@@ -64,11 +64,26 @@ constexpr uint32_t BVH_LEAF_BIT = 0x80000000u;
 #endif
 constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (LDS); overflow -> exact full scan
 
-// Kernel arguments (passed by value in the kernarg segment).
-struct KParams {
+// Small culling BVHs (<= LNODE_CAP nodes, depth <= LNODE_DEPTH) are read from LDS by k_trace_split<true>
+// (renderer.cpp decides, the kernel bounds its copy by the same constant).
+constexpr uint32_t LNODE_CAP = 192;
+constexpr uint32_t LNODE_DEPTH = 8;
+
+// Camera-derived constants of make_ray / fs_main, read only when primary rays are generated (once per frame
+// block in the sample queue). The kernels read them through kargs() (below), a pointer to the kernarg segment
+// the compiler cannot see through, so the loads stay where they are used instead of being hoisted to the
+// kernel entry and kept in SGPRs across the persistent loops (round-1 code objects kept these 28 values
+// resident and spilled 51-54 SGPRs to VGPR lanes in k_trace_split).
+struct CamDev {
     float eye[4], dir[4], up[4], right[4];
     float focal, blur, k;         // k = tan(fov / 2), host libm tanf
     float aspect, wm1, hm1;       // f32(W)/f32(H), f32(W) - 1, f32(H) - 1 (host, same IEEE ops)
+    uint32_t H, pad;
+};
+
+// Kernel arguments (passed by value in the kernarg segment).
+struct KParams {
+    CamDev cam;                   // make_ray constants (read through kargs())
     uint32_t W, H;
     uint32_t time0, dtime, frame0, nframes;
     uint32_t bounces;
@@ -93,7 +108,7 @@ struct KParams {
                                   // renderer.cpp pack_bvh_hnodes); bvh_nodes is the f32 form (bvh_run<.., false>)
     float bvh_rr_h;               // radius bound of the fp16 boxes (>= their half-diagonal)
     uint32_t bvh_nnodes;          // nodes in bvh_hnodes
-    uint32_t bvh_lnodes, pad_ln;  // 1: k_trace_split keeps the nodes in LDS (<= 192 nodes, depth <= 8)
+    uint32_t bvh_lnodes, pad_ln;  // 1: k_trace_split keeps the nodes in LDS (<= LNODE_CAP nodes, depth <= 8)
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp), nodes with fp16 boxes like bvh_hnodes
     const uint32_t* tb_order;     // triangle index of each leaf entry
@@ -115,6 +130,17 @@ struct KParams {
     uint32_t suspend_below;       // k_trace_split: suspend the walks once fewer lanes than this still walk
     uint32_t pad_q;
 };
+
+// KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot
+// trace back to the kernel's entry, so every use is a fresh s_load (K$) instead of a live SGPR.
+typedef const __attribute__((address_space(4))) KParams* KPtr;
+typedef const __attribute__((address_space(4))) CamDev* CamPtr;
+__device__ __forceinline__ KPtr kargs() {
+    const unsigned long long v = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (KPtr)(((unsigned long long)hi << 32) | lo);
+}
 
 struct f3 {
     float x, y, z;

@@ -788,32 +788,32 @@ __device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
 
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
 template <int MODE>
-__device__ __forceinline__ Ray primary_ray(const KParams& P, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
-    s = (x * P.H + y) * time;
+__device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
+    s = (x * C->H + y) * time;
     const float r1 = rng_float(s);
     const float r2 = rng_float(s);
     const float l = __builtin_sqrtf(__builtin_fmaf(r2, r2, r1 * r1));
     const float px = ((float)x + 0.5f) + r1 / l;
     const float py = ((float)y + 0.5f) + r2 / l;
-    const float ux = (2.0f * (px / P.wm1) - 1.0f) * P.aspect;
-    const float uy = (2.0f * (py / P.hm1) - 1.0f) * -1.0f;
+    const float ux = (2.0f * (px / C->wm1) - 1.0f) * C->aspect;
+    const float uy = (2.0f * (py / C->hm1) - 1.0f) * -1.0f;
     float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) v[i] = ((P.right[i] * ux) * P.k + (P.up[i] * uy) * P.k) + P.dir[i];
+    for (int i = 0; i < 4; i++) v[i] = ((C->right[i] * ux) * C->k + (C->up[i] * uy) * C->k) + C->dir[i];
     const float lv = __builtin_sqrtf(__builtin_fmaf(v[3], v[3], __builtin_fmaf(v[2], v[2], __builtin_fmaf(v[1], v[1], v[0] * v[0]))));
     float f4[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) f4[i] = P.eye[i] + (v[i] / lv) * P.focal;
+    for (int i = 0; i < 4; i++) f4[i] = C->eye[i] + (v[i] / lv) * C->focal;
     // random_on_disk (:118-122): +x,+y quadrant unit vector times rng*radius, in world xy.
     const float q1 = rng_float(s);
     const float q2 = rng_float(s);
     const float lq = __builtin_sqrtf(__builtin_fmaf(q2, q2, q1 * q1));
-    const float rr = rng_float(s) * P.blur;
+    const float rr = rng_float(s) * C->blur;
     float o4[4];
-    o4[0] = P.eye[0] + (q1 / lq) * rr;
-    o4[1] = P.eye[1] + (q2 / lq) * rr;
-    o4[2] = P.eye[2] + 0.0f * rr;
-    o4[3] = P.eye[3] + 1.0f;
+    o4[0] = C->eye[0] + (q1 / lq) * rr;
+    o4[1] = C->eye[1] + (q2 / lq) * rr;
+    o4[2] = C->eye[2] + 0.0f * rr;
+    o4[3] = C->eye[3] + 1.0f;
     Ray r;
     r.o = mk(o4[0], o4[1], o4[2]);
     if (MODE == MODE_SPHERE) {
@@ -904,7 +904,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bo
             B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             if (B.pr_ok) {
                 const uint32_t y = P.row0 + kr * P.row_step;
-                const Ray pr = primary_ray<MODE>(P, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
+                const Ray pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
                 B.pr_o = pr.o;
                 B.pr_d = pr.d;
             }
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     float sky_t = 0.0f;
     uint32_t s = 0, bounce = 0;
     if (f < P.nframes) {
-        ray = primary_ray<MODE>(P, x, y, P.time0, s);
+        ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0, s);
         sky_t = ray.d.y * 0.5f + 0.5f;
     }
 
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
             acc2 = acc2 * omw + (0.0f + c.z) * w;
             f++;
             if (f < P.nframes) {
-                ray = primary_ray<MODE>(P, x, y, P.time0 + f * P.dtime, s);
+                ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + f * P.dtime, s);
                 sky_t = ray.d.y * 0.5f + 0.5f;
                 att = mk(1.0f, 1.0f, 1.0f);
                 bounce = 0;
@@ -1169,7 +1169,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 need = false;
                 if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
                     const uint32_t y = P.row0 + kr * P.row_step;
-                    ray = primary_ray<MODE>(P, x, y, P.time0 + fl * P.dtime, s);
+                    ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + fl * P.dtime, s);
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
                     bounce = 0;
@@ -1216,7 +1216,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             const float u = 1.0f - sky_t;
             const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
             const f3 c = att * sky;
-            float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
+            const KPtr K = kargs();
+            float* o = K->samples + ((size_t)fl * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
@@ -1279,31 +1280,32 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
     unsigned long long m = __ballot(need);
     while (m != 0ull) {
         if (B.blk_next == 64u) {
+            const KPtr K = kargs();  // queue and camera constants: loaded here, not held in SGPRs
             if (B.blk_f + 1u < B.job_nf) {
                 B.blk_f++;
             } else {
                 unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(P.queue, 1ull);
+                if (lane == 0) j = atomicAdd(K->queue, 1ull);
                 j = __shfl(j, 0);
-                if (j >= P.njobs) {
+                if (j >= K->njobs) {
                     drained = true;
                     break;
                 }
-                const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                B.job_tile = (uint32_t)(j / P.nchunks);
-                B.job_f0 = chunk * P.job_frames;
-                B.job_nf = min(P.job_frames, P.nframes - B.job_f0);
+                const uint32_t chunk = (uint32_t)(j % K->nchunks);
+                B.job_tile = (uint32_t)(j / K->nchunks);
+                B.job_f0 = chunk * K->job_frames;
+                B.job_nf = min(K->job_frames, K->nframes - B.job_f0);
                 B.blk_f = 0;
             }
             B.blk_next = 0;
-            const uint32_t x = (B.job_tile % P.tiles_w) * 8u + (lane & 7u);
-            const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
-            const uint32_t pok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
+            const uint32_t x = (B.job_tile % K->tiles_w) * 8u + (lane & 7u);
+            const uint32_t kr = (B.job_tile / K->tiles_w) * 8u + (lane >> 3);
+            const uint32_t pok = (x < K->W && kr < K->nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
             uint32_t ps = 0;
             if (pok) {
-                const uint32_t y = P.row0 + kr * P.row_step;
-                pr = primary_ray<MODE>(P, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, ps);
+                const uint32_t y = K->row0 + kr * K->row_step;
+                pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
             }
             blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
             blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
@@ -1350,16 +1352,16 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
 // LNODES (small trees: <= LNODE_CAP nodes, depth <= 8): the fp16 nodes are copied into LDS once per
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
-constexpr int LNODE_CAP = 192;
 template <bool LNODES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
-    constexpr int SPLIT_STACK = LNODES ? 8 : 14;
+    constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
     const uint32_t lane = threadIdx.x & 63u;
     __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
     __shared__ uint4 lnodes[LNODES ? 2 * LNODE_CAP : 1];
     if constexpr (LNODES) {
-        for (uint32_t i = threadIdx.x; i < 2u * P.bvh_nnodes; i += 256u) lnodes[i] = P.bvh_hnodes[i];
+        const uint32_t nn = 2u * min(P.bvh_nnodes, LNODE_CAP);  // renderer.cpp gates LNODES on the same cap
+        for (uint32_t i = threadIdx.x; i < nn; i += 256u) lnodes[i] = P.bvh_hnodes[i];
         __syncthreads();
     }
     __shared__ float4 blk[2 * 256];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
@@ -1411,7 +1413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 uint32_t ps = 0;
                 if (pok) {
                     const uint32_t y = P.row0 + kr * P.row_step;
-                    pr = primary_ray<MODE>(P, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, ps);
+                    pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, ps);
                 }
                 blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
                 blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
@@ -1601,7 +1603,8 @@ k_trace_split_tris(const KParams P) {
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
+                const KPtr K = kargs();
+                float* o = K->samples + ((size_t)fl * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
                 o[0] = c.x;
                 o[1] = c.y;
                 o[2] = c.z;
