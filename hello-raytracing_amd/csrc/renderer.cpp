@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -24,6 +25,7 @@ hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, h
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 const char* hrt_last_kernel();
+hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
 
 namespace {
 
@@ -61,8 +63,15 @@ int ensure(DevBuf<T>& b, size_t n) {
     if (n <= b.cap && b.ptr) return RT_OK;
     b.release();
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    // fault injection for tests: HRT_FAIL_ALLOC_ABOVE_MB=m makes every device allocation above m MiB fail
+    static const char* cap_env = std::getenv("HRT_FAIL_ALLOC_ABOVE_MB");
+    if (cap_env && bytes > ((size_t)std::strtoull(cap_env, nullptr, 10) << 20))
+        return fail(RT_ERR_ALLOC, "hipMalloc: injected failure (HRT_FAIL_ALLOC_ABOVE_MB)");
     hipError_t e = hipMalloc((void**)&b.ptr, bytes);
-    if (e != hipSuccess) return fail(RT_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        b.ptr = nullptr;
+        return fail(RT_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
     b.cap = std::max<size_t>(n, 1);
     return RT_OK;
 }
@@ -432,9 +441,14 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.tiles_h = (P.nrows + 7u) / 8u;
         const size_t frame_floats = (size_t)P.tiles_w * P.tiles_h * 64u * 3u;  // tile-padded
         const size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
-        const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+        uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
         if (count) {
-            rc = ensure(r->samples, (size_t)chunk * frame_floats);
+            // a device short of memory (another process, a smaller part) gets smaller chunks, down to one frame,
+            // instead of a failed draw
+            while ((rc = ensure(r->samples, (size_t)chunk * frame_floats)) == RT_ERR_ALLOC && chunk > 1u) {
+                (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
+                chunk = (chunk + 1u) / 2u;
+            }
             if (rc) return rc;
         }
         P.samples = r->samples.ptr;
@@ -783,6 +797,21 @@ int rt_get_wave_trace(rt_renderer* r, uint64_t* out, size_t n_words) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_get_wave_trace: null");
     if (n_words > r->wave_trace_words) return fail(RT_ERR_ARG, "rt_get_wave_trace: more words than recorded");
     if (n_words) HIP_TRY(hipMemcpy(out, r->wave_trace.ptr, n_words * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]) {
+    if (!mismatches) return fail(RT_ERR_ARG, "rt_check_exact_math: null");
+    int dev = 0;
+    int rc = check_device(&dev);
+    if (rc) return rc;
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 3 * sizeof(unsigned long long)));
+    hipError_t e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hrt_check_exact_math(n, seed, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(mismatches, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("rt_check_exact_math: ") + hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -166,6 +166,41 @@ __device__ __forceinline__ f3 point_on_ray(f3 o, f3 d, float t) {
 __device__ __forceinline__ float fmin_ieee(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ float fmax_ieee(float a, float b) { return __builtin_fmaxf(a, b); }
 
+// Correctly rounded sqrt for x in [2^-100, 2^100] or x == 0: v_sqrt_f32 (<= 1 ulp) then the Tuckerman
+// rounding test that the HIP library sequence applies (one ulp down / up, chosen by the sign of the exact FMA
+// residual), without that sequence's denormal scaling and special-class fix-up, which such x never need.
+__device__ __forceinline__ float sqrt_rn_mid(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    const float t = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : t;
+}
+
+// Correctly rounded x / l for several x sharing one divisor: v_rcp_f32 refined by one Newton step, then
+// q = x r and two exact-residual corrections (the FMA steps of the HIP division sequence, whose
+// v_div_scale / v_div_fmas / v_div_fixup only handle operands near the ends of the range). Valid when l
+// and every nonzero |x| lie in [2^-60, 2^60] (all intermediates normal, residuals exact); x = +0 gives +0.
+struct RcpRN {
+    float l, r;
+};
+__device__ __forceinline__ RcpRN rcp_rn_setup(float l) {
+    const float r0 = __builtin_amdgcn_rcpf(l);
+    return RcpRN{l, __builtin_fmaf(__builtin_fmaf(-l, r0, 1.0f), r0, r0)};
+}
+__device__ __forceinline__ float div_rn_mid(float x, const RcpRN& d) {
+    float q = x * d.r;
+    q = __builtin_fmaf(__builtin_fmaf(-d.l, q, x), d.r, q);
+    return __builtin_fmaf(__builtin_fmaf(-d.l, q, x), d.r, q);
+}
+
+// normalize() of a vector of rng floats (each 0 or in [2^-32, 1], not all 0): dot in [2^-64, 3], so the
+// length and the three quotients stay inside the ranges above; bit-identical to normalize().
+__device__ __forceinline__ f3 normalize_rng(f3 a) {
+    const RcpRN d = rcp_rn_setup(sqrt_rn_mid(dot(a, a)));
+    return mk(div_rn_mid(a.x, d), div_rn_mid(a.y, d), div_rn_mid(a.z, d));
+}
+
 // PCG hash step — shader_sphere.wgsl:87-93.
 __device__ __forceinline__ uint32_t pcg_next(uint32_t s) {
     uint32_t old = s + 747796405u + 2891336453u;

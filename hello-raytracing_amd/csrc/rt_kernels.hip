@@ -748,7 +748,8 @@ __device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
     const float x = rng_float(s);
     const float y = rng_float(s);
     const float z = rng_float(s);
-    const f3 v = normalize(mk(x, y, z));
+    // normalize() with the range-restricted exact sequences (rt_device.hpp normalize_rng): 30 instead of 52 VALU
+    const f3 v = normalize_rng(mk(x, y, z));
     // `length(v) < EPSILON` (:110) never holds here, so it is not evaluated: x, y, z are rng floats in
     // [0, 1]; either all are 0 (v = NaN, and NaN < EPS is false) or the largest is >= 2^-32, dot(v, v) is a
     // normal float and the normalised v has length >= 0.577. The oracle keeps the test; parity compares.
@@ -1651,6 +1652,46 @@ __global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
     px[0] = acc0;
     px[1] = acc1;
     px[2] = acc2;
+}
+
+// Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE
+// operations (correctly rounded in this build): n random cases per test, counted mismatches in out[0..2]:
+// [0] normalize_rng vs normalize on vectors of rng floats (the hemisphere sample), [1] div_rn_mid vs `/` on
+// log-uniform operands in [2^-60, 2^60] (random signs, and x = 0), [2] sqrt_rn_mid vs sqrtf on [2^-100, 2^100].
+__global__ __launch_bounds__(256) void k_check_exact_math(unsigned long long n, uint32_t seed,
+                                                          unsigned long long* out) {
+    unsigned long long bad[3] = {0, 0, 0};
+    const unsigned long long stride = (unsigned long long)gridDim.x * 256u;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256u + threadIdx.x; i < n; i += stride) {
+        uint32_t s = (uint32_t)i * 2654435761u ^ seed ^ (uint32_t)(i >> 32) * 40503u;
+        const f3 v = mk(rng_float(s), rng_float(s), rng_float(s));
+        const f3 a = normalize(v), b = normalize_rng(v);
+        if (__float_as_uint(a.x) != __float_as_uint(b.x) || __float_as_uint(a.y) != __float_as_uint(b.y) ||
+            __float_as_uint(a.z) != __float_as_uint(b.z))
+            bad[0]++;
+        // log-uniform magnitudes: exponent in [-60, 60), random mantissa and sign
+        s = pcg_next(s);
+        const uint32_t ex = 67u + (s % 120u), ey = 67u + ((s >> 8) % 120u);
+        const uint32_t mx = pcg_next(s), my = pcg_next(mx);
+        float x = __uint_as_float((ex << 23) | (mx & 0x7FFFFFu) | (mx & 0x80000000u));
+        const float l = __uint_as_float((ey << 23) | (my & 0x7FFFFFu) | (my & 0x80000000u));
+        if ((mx & 0xFFu) == 0u) x = 0.0f;
+        if (__float_as_uint(x / l) != __float_as_uint(div_rn_mid(x, rcp_rn_setup(l)))) bad[1]++;
+        const uint32_t es = 27u + (my % 200u);
+        const float q = __uint_as_float((es << 23) | (pcg_next(my) & 0x7FFFFFu));
+        if (__float_as_uint(__builtin_sqrtf(q)) != __float_as_uint(sqrt_rn_mid(q))) bad[2]++;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) bad[c] += __shfl_xor(bad[c], off);
+        if ((threadIdx.x & 63u) == 0 && bad[c]) atomicAdd(out + c, bad[c]);
+    }
+}
+
+hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st) {
+    hipLaunchKernelGGL(k_check_exact_math, dim3(4096), dim3(256), 0, st, n, seed, out_dev);
+    return hipGetLastError();
 }
 
 // Demangled-symbol form of the kernel a draw ran ("k_trace_split<true>"): rt_stats.kernel, and the key

@@ -92,6 +92,7 @@ SIGNATURES = {
     "rt_get_stats": (C.c_int, [_P, C.POINTER(RtStats)]),
     "rt_get_raw_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "rt_diagnostic_build": (C.c_int, []),
+    "rt_check_exact_math": (C.c_int, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "rt_get_wave_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_last_error": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),

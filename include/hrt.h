@@ -163,6 +163,11 @@ int rt_diagnostic_build(void);
  * XCC_ID << 32, closest-hit queries of the wave. Zero words in the product build. */
 int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 
+/* Self-check of the kernels' range-restricted correctly rounded sqrt / division sequences against the IEEE
+ * operations on n random cases each (diagnostics): mismatches[0] normalize of rng
+ * vectors, [1] division on [2^-60, 2^60], [2] sqrt on [2^-100, 2^100]. All three must be 0. */
+int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]);
+
 /* Thread-local message for the last failing call. */
 const char *rt_last_error(void);
 /* Number of visible gfx950 devices (0 on a CPU-only host; never an error). */

@@ -180,6 +180,36 @@ def test_sample_queue_chunks_and_tris_mode():
     assert_parity(imgs[1], ref_img, "suzane tris, queue schedule")
 
 
+def test_sample_buffer_allocation_failure_halves_the_chunk():
+    """A colour-buffer allocation the device refuses (fault injection: every allocation above 100 MiB fails
+    in a subprocess with HRT_FAIL_ALLOC_ABOVE_MB=100): the renderer halves the chunk until one fits and the
+    draw completes, bit-identical to the default single-chunk draw."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path[:0] = ['hello-raytracing_amd', 'tests']; import numpy as np, scenes, hrt\n"
+            "sd = scenes.golden_scene('metal_materials', 512, 512); r = scenes.make_renderer(sd)\n"
+            "r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE); r.draw_frames(40, 1000, 10)\n"
+            "np.save(sys.argv[1], r.read_image()); print(r.stats().launches)\n")
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    out = root / "tests" / "output"
+    out.mkdir(exist_ok=True)
+    import os
+    env = dict(os.environ, HRT_FAIL_ALLOC_ABOVE_MB="100")
+    p = subprocess.run([sys.executable, "-c", code, str(out / "alloc_small.npy")], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert int(p.stdout.split()[-1]) >= 4  # 40 frames x 3 MiB do not fit in 100 MiB: at least two chunks
+    sd = scenes.golden_scene("metal_materials", 512, 512)
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE)
+    r.draw_frames(40, 1000, 10)
+    assert r.stats().launches == 2
+    small = np.load(out / "alloc_small.npy")
+    np.testing.assert_array_equal(small.view(np.uint32), r.read_image().view(np.uint32))
+
+
 def test_query_count_matches_oracle():
     sd = scenes.golden_scene("dielectric_materials", 64, 48)
     r = scenes.make_renderer(sd)
@@ -651,6 +681,17 @@ def test_rendering_performance():
     elapsed = time.perf_counter() - t0
     assert elapsed < 5.0, f"Rendering took too long: {elapsed:.3f} s"
     assert np.isfinite(scene.renderer.read_image()).all()
+
+
+def test_range_restricted_exact_math_matches_ieee():
+    """The kernels' short correctly rounded sequences (hemisphere normalize, division by a shared refined
+    reciprocal, sqrt without scaling; rt_device.hpp) equal the IEEE operations bit for bit on 2^30 random
+    cases each in their stated ranges."""
+    import ctypes as C
+    out = (C.c_uint64 * 3)()
+    for seed in (1, 0x9E3779B9):
+        hrt._lib.check(hrt.lib().rt_check_exact_math(1 << 30, seed, out), "rt_check_exact_math")
+        assert list(out) == [0, 0, 0], list(out)
 
 
 def test_bad_arguments_fail_loudly():
