@@ -37,11 +37,11 @@ for f in sorted(glob.glob(f"{out}/**/p*_counter_collection.csv", recursive=True)
     for r in csv.DictReader(open(f)):
         if symbol(r["Kernel_Name"]) != kernel:
             continue
-        key = (f, r["Dispatch_Id"])
-        per[key][r["Counter_Name"]] += float(r["Counter_Value"])
-        names[key] = r["Kernel_Name"]
+        dk = (f, r["Dispatch_Id"])
+        per[dk][r["Counter_Name"]] += float(r["Counter_Value"])
+        names[dk] = r["Kernel_Name"]
 agg = collections.defaultdict(list)
-for key, cs in per.items():
+for dk, cs in per.items():
     for c, v in cs.items():
         agg[c].append(v)
 summary = {c: sum(v) / len(v) for c, v in agg.items()}
