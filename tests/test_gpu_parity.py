@@ -470,13 +470,15 @@ def _random_scene(kind: str, seed: int):
                            min_sphere_slots=0)
 
 
+@pytest.mark.parametrize("schedule", [1, 2])
 @pytest.mark.parametrize("kind", ["tangent_grid", "radius_spread", "far_offset"])
-def test_culling_bvh_exact_on_adversarial_scenes(kind):
+def test_culling_bvh_exact_on_adversarial_scenes(kind, schedule):
+    """Tiles (k_render) and the sample queue (k_trace_split; nodes in LDS: these trees have < 192 nodes)."""
     sd = _random_scene(kind, 7)
     out = []
     for variant in (1, 4):
         r = scenes.make_renderer(sd)
-        r.set_params(variant=variant, schedule=1)
+        r.set_params(variant=variant, schedule=schedule)
         r.draw_frames(sd.frames, 1000, 10)
         out.append((r.read_image(), r.stats()))
     for (img, st), v in zip(out[1:], (4,)):
