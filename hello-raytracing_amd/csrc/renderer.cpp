@@ -155,6 +155,17 @@ struct rt_renderer {
 
 namespace {
 
+// The dielectric scatter arm's per-hit divisions, done once per material with the kernels' f32 operations
+// (shader_sphere.wgsl:185-199: ir = 1 / params.x on a front face; reflectance's r0 = (1 - ir) / (1 + ir)).
+hrt_dev::DielConsts dielectric_consts(float param) {
+    auto r0sq = [](float ir) {
+        const float r0 = (1.0f - ir) / (1.0f + ir);
+        return r0 * r0;
+    };
+    const float inv = 1.0f / param;
+    return hrt_dev::DielConsts{inv, r0sq(inv), r0sq(param)};
+}
+
 int zero_image(rt_renderer* r) {
     int rc = ensure(r->image, r->image_floats());
     if (rc) return rc;
@@ -239,13 +250,22 @@ int upload_spheres(rt_renderer* r) {
     std::vector<float4> geo(nslots, float4{0.0f, 0.0f, 0.0f, 0.0f});
     std::vector<hrt_dev::SphereAux> aux(nslots);
     std::memset(aux.data(), 0, aux.size() * sizeof(aux[0]));
+    for (uint32_t i = (uint32_t)r->spheres.size(); i < nslots; i++) {  // zero slots: params 0, id 0 (default arm)
+        const hrt_dev::DielConsts dc = dielectric_consts(0.0f);
+        aux[i].inv_param = dc.inv_param;
+        aux[i].r0sq_front = dc.r0sq_front;
+        aux[i].r0sq_back = dc.r0sq_back;
+    }
     for (size_t i = 0; i < r->spheres.size(); i++) {
         const hrt::Sphere& s = r->spheres[i];
         const float rr = s.radius * s.radius;  // radius*radius, shader_sphere.wgsl:142
         geo[i] = float4{s.center.x, s.center.y, s.center.z, rr};
+        const hrt_dev::DielConsts dc = dielectric_consts(s.material.params.x);
+        const bool rad_ok = std::fabs(s.radius) >= 0x1p-60f && std::fabs(s.radius) <= 0x1p60f;
         aux[i] = hrt_dev::SphereAux{s.center.x, s.center.y, s.center.z, s.radius,
                                     s.material.albedo.x, s.material.albedo.y, s.material.albedo.z,
-                                    s.material.params.x, s.material.kind, 0, 0, 0};
+                                    s.material.params.x, s.material.kind, dc.inv_param, dc.r0sq_front, dc.r0sq_back,
+                                    rad_ok ? 1.0f / s.radius : 0.0f, 0.0f, 0.0f, 0.0f};
     }
     // slot pairs for the packed scan; an odd tail slot is paired with a NaN-centre slot (never accepted)
     const uint32_t npairs = (nslots + 1) / 2;
@@ -648,6 +668,8 @@ int rt_set_camera(rt_renderer* r, const void* camera80) {
 
 int rt_set_spheres(rt_renderer* r, const void* spheres48, uint32_t n) {
     if (!r || (n && !spheres48)) return fail(RT_ERR_ARG, "rt_set_spheres: null");
+    // a hit carries its slot in 29 bits (rt_kernels.hip Hit::id)
+    if (n >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_spheres: more than 2^28 spheres");
     r->spheres.resize(n);
     if (n) std::memcpy(r->spheres.data(), spheres48, (size_t)n * sizeof(hrt::Sphere));
     return upload_spheres(r);
@@ -661,6 +683,7 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
     if ((n && !nodes32) || (m && !tris64) || (n_mats && !mats32)) return fail(RT_ERR_ARG, "rt_set_bvh: null buffer");
     if (n > (1u << 30)) return fail(RT_ERR_ARG, "rt_set_bvh: tree too large");
+    if (n_mats >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_bvh: more than 2^28 materials");
     const hrt::Triangle* T = (const hrt::Triangle*)tris64;
     std::vector<hrt_dev::TriDev> td(m);
     for (uint32_t j = 0; j < m; j++) {
@@ -686,7 +709,11 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     const hrt::Material* M = (const hrt::Material*)mats32;
     std::vector<hrt_dev::MatDev> md(n_mats);
     for (uint32_t k = 0; k < n_mats; k++)
-        md[k] = hrt_dev::MatDev{M[k].albedo.x, M[k].albedo.y, M[k].albedo.z, M[k].params.x, M[k].kind, 0, 0, 0};
+    {
+        const hrt_dev::DielConsts dc = dielectric_consts(M[k].params.x);
+        md[k] = hrt_dev::MatDev{M[k].albedo.x, M[k].albedo.y, M[k].albedo.z, M[k].params.x, M[k].kind,
+                                dc.inv_param, dc.r0sq_front, dc.r0sq_back};
+    }
     int rc = ensure(r->nodes, 2 * (size_t)std::max<uint32_t>(n, 1));
     if (!rc) rc = ensure(r->tris, std::max<uint32_t>(m, 1));
     if (!rc) rc = ensure(r->mats, std::max<uint32_t>(n_mats, 1));

@@ -18,13 +18,23 @@ namespace hrt_dev {
 constexpr float FLT_MAX_REF = 3.40282e+38f;  // shader_*.wgsl:4
 constexpr int MODE_SPHERE = 0, MODE_TRIS = 1, MODE_MIXED = 2;
 
-// Winner-only sphere data (loaded once per query, for the closest sphere).
+// Dielectric constants the scatter arm would otherwise derive per hit with two IEEE divisions, computed on
+// the host with the same f32 operations (renderer.cpp dielectric_consts): 1 / param (the ratio of a
+// front-face hit) and reflectance's r0 * r0 for ir = 1 / param (front) and ir = param (back).
+struct DielConsts {
+    float inv_param, r0sq_front, r0sq_back;
+};
+
+// Winner-only sphere data (loaded once per query, for the closest sphere). inv_radius = RN(1 / radius) when
+// radius lies in [2^-60, 2^60] (else 0: the hit normal divides exactly by radius the slow way).
 struct SphereAux {
     float cx, cy, cz, radius;
     float ar, ag, ab, param;  // albedo.rgb, params.x
-    uint32_t id, pad0, pad1, pad2;
+    uint32_t id;
+    float inv_param, r0sq_front, r0sq_back;  // DielConsts
+    float inv_radius, pad0, pad1, pad2;
 };
-static_assert(sizeof(SphereAux) == 48, "SphereAux");
+static_assert(sizeof(SphereAux) == 64, "SphereAux");
 
 // Triangle as the kernel reads it: a, e1 = b - a, e2 = c - a (host-precomputed with the same f32
 // subtraction Moller-Trumbore performs, shader_tris.wgsl:168-169), stored normal + material index.
@@ -39,7 +49,8 @@ static_assert(sizeof(TriDev) == 64, "TriDev");
 
 struct MatDev {
     float ar, ag, ab, param;
-    uint32_t id, pad0, pad1, pad2;
+    uint32_t id;
+    float inv_param, r0sq_front, r0sq_back;  // DielConsts
 };
 static_assert(sizeof(MatDev) == 32, "MatDev");
 
@@ -225,6 +236,12 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {
 __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {
     float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
     r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    float x2 = x * x;
+    return r0 + (1.0f - r0) * ((x2 * x2) * x);
+}
+// reflectance() with r0 * r0 precomputed (the same f32 operations, on the host).
+__device__ __forceinline__ float reflectance_r0sq(float cosine, float r0) {
     float x = 1.0f - cosine;
     float x2 = x * x;
     return r0 + (1.0f - r0) * ((x2 * x2) * x);

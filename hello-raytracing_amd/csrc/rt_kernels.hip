@@ -51,6 +51,8 @@ struct Hit {
     f3 p, n;
     float t;
     float ar, ag, ab, param;
+    // material arm in bits 0-1 (1 lambertian, 2 metal, 0 dielectric / default), bit 2 set for a sphere hit,
+    // and above them the sphere slot (sph_aux) or material index (mats) the dielectric constants are read from
     uint32_t id;
     bool front;
 };
@@ -453,18 +455,28 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
     return bvh_end(P, r, Q, best, tally);
 }
 
+// (p - c) / radius, exact: the host's correctly rounded 1 / radius and two residual corrections
+// (div_rn_mid) where the numerator's magnitude keeps the residuals exact, the IEEE division elsewhere (zero,
+// tiny or huge components, radius outside [2^-60, 2^60]: inv_radius = 0).
+__device__ __forceinline__ float div_by_radius(float x, float radius, float inv_radius) {
+    const float ax = __builtin_fabsf(x);
+    if (inv_radius != 0.0f && ax >= 0x1p-100f && ax <= 0x1p60f) return div_rn_mid(x, RcpRN{radius, inv_radius});
+    return x / radius;
+}
+
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
     const f3 p = point_on_ray(r.o, r.d, t);
     f3 n = p - mk(s.cx, s.cy, s.cz);
-    n = mk(n.x / s.radius, n.y / s.radius, n.z / s.radius);
+    n = mk(div_by_radius(n.x, s.radius, s.inv_radius), div_by_radius(n.y, s.radius, s.inv_radius),
+           div_by_radius(n.z, s.radius, s.inv_radius));
     const bool front = dot(r.d, n) < 0.0f;
     if (!front) n = -n;
     h.p = p;
     h.n = n;
     h.t = t;
     h.ar = s.ar; h.ag = s.ag; h.ab = s.ab; h.param = s.param;
-    h.id = s.id;
+    h.id = ((uint32_t)bi << 3) | 4u | (s.id == 1u || s.id == 2u ? s.id : 0u);
     h.front = front;
 }
 
@@ -503,7 +515,7 @@ __device__ __forceinline__ void tri_record(const KParams& P, const Ray& r, const
     h.n = mk(tr.nx, tr.ny, tr.nz);
     h.t = t;
     h.ar = m.ar; h.ag = m.ag; h.ab = m.ab; h.param = m.param;
-    h.id = m.id;
+    h.id = (tr.material << 3) | (m.id == 1u || m.id == 2u ? m.id : 0u);
     h.front = dot(h.n, r.d) > 0.0f;
 }
 
@@ -763,8 +775,8 @@ __device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
 // one final normalize instead of one per arm; every lane still performs exactly its own arm's operations
 // (and RNG draws) in the reference's order, so results are unchanged.
 template <int MODE>
-__device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
-    const bool lambert = h.id == 1u, metal = h.id == 2u;
+__device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, const Hit& h) {
+    const bool lambert = (h.id & 3u) == 1u, metal = (h.id & 3u) == 2u;
     f3 hemi = mk(0.0f, 0.0f, 0.0f);
     if (lambert || metal) hemi = random_on_hemisphere<MODE>(s, h.n);  // 3 draws, both arms
     f3 u = hemi;
@@ -772,14 +784,16 @@ __device__ __forceinline__ void scatter(uint32_t& s, Ray& r, const Hit& h) {
         const f3 in = MODE == MODE_SPHERE ? normalize(r.d) : r.d;
         u = reflect(in, h.n) + h.param * hemi;
     } else if (!lambert) {  // MAT_DIELECTRIC and the default arm
-        float ir = h.param;
-        if (h.front) ir = 1.0f / ir;
+        // ir = front ? 1 / param : param, and reflectance's r0 * r0 for that ir, from the host (DielConsts)
+        const float* dc = (MODE == MODE_SPHERE || (MODE != MODE_TRIS && (h.id & 4u))) ? &P.sph_aux[h.id >> 3].inv_param
+                                                                                     : &P.mats[h.id >> 3].inv_param;
+        const float ir = h.front ? dc[0] : h.param;
         const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
         const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
         bool refl = ir * sin_t > 1.0f;  // cannot_refract; WGSL || short-circuits the RNG draw
         if (!refl) {
             const float f = rng_float(s);
-            refl = reflectance(cos_t, ir) > (f - __builtin_floorf(f));
+            refl = reflectance_r0sq(cos_t, h.front ? dc[1] : dc[2]) > (f - __builtin_floorf(f));
         }
         u = refl ? reflect(r.d, h.n) : refract(r.d, h.n, ir);
     }
@@ -992,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
             st_trav += st_tb - st_ta;
 #endif
             if (hit) {
-                scatter<MODE>(s, ray, h);
+                scatter<MODE>(P, s, ray, h);
                 att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                 bounce++;
                 done = bounce >= P.bounces;
@@ -1206,7 +1220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             st_tb = st_ta;
 #endif
             if (hit) {
-                scatter<MODE>(s, ray, h);
+                scatter<MODE>(P, s, ray, h);
                 att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                 bounce++;
                 done = bounce >= P.bounces;
@@ -1479,7 +1493,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 if (bi >= 0) {
                     Hit h;
                     sphere_record(P, ray, bi, best, h);
-                    scatter<MODE>(s, ray, h);
+                    scatter<MODE>(P, s, ray, h);
                     att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                     bounce++;
                     done = bounce >= P.bounces;
@@ -1594,7 +1608,7 @@ k_trace_split_tris(const KParams P) {
                 else if (bi >= 0) sphere_record(P, ray, bi, W.best, h);
                 else hit = false;
                 if (hit) {
-                    scatter<MODE>(s, ray, h);
+                    scatter<MODE>(P, s, ray, h);
                     att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                     bounce++;
                     done = bounce >= P.bounces;
