@@ -23,7 +23,6 @@
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
-hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 const char* hrt_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
 
@@ -129,7 +128,8 @@ struct rt_renderer {
     DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
-    DevBuf<float> samples;  // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major
+    DevBuf<float4> ring;        // sample-queue fold ring: slots x frames x 64 px (rgb, unused)
+    DevBuf<uint32_t> ring_ctl;  // [0, slots): jobs completed per slot; [slots, 2 slots): folds per slot
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
 
@@ -143,6 +143,7 @@ struct rt_renderer {
     uint32_t trace_pairs = 0;
     uint32_t last_schedule = 0;
     uint32_t last_suspend = 0;
+    uint32_t ring_slots = 0;  // fold-ring slots of the last sample-queue draw
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
@@ -456,23 +457,44 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 
     uint32_t launches = 0;
     if (schedule == RT_SCHEDULE_QUEUE) {
-        // frames per chunk: as many as the colour buffer budget holds
         P.tiles_w = (r->width + 7u) / 8u;
         P.tiles_h = (P.nrows + 7u) / 8u;
-        const size_t frame_floats = (size_t)P.tiles_w * P.tiles_h * 64u * 3u;  // tile-padded
-        const size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
-        uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+        const uint32_t ntiles = P.tiles_w * P.tiles_h;
+        // fold ring: a slot (frames x 64 px x 16 B) per tile in flight. Frames per launch: as many as leave room
+        // for RING_MIN_SLOTS slots in the budget; slots: a power of two, at most one per tile. A device short of
+        // memory gets a halved budget (fewer slots, then fewer frames per launch) instead of a failed draw.
+        constexpr uint32_t RING_MIN_SLOTS = 256;
+        size_t budget = (size_t)std::min<uint32_t>(std::max<uint32_t>(r->params.queue_budget_mb, 1u), 2047u) << 20;
+        uint32_t chunk = 1, log2s = 0;
+        auto plan = [&]() {
+            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / ((size_t)RING_MIN_SLOTS << 10)));
+            const size_t fit = std::max<size_t>(1, budget / ((size_t)chunk << 10));
+            log2s = 0;
+            while ((2ull << log2s) <= fit && (1ull << log2s) < ntiles) log2s++;
+            // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so tiles wait for their slot
+            static const char* cap_env = std::getenv("HRT_RING_SLOTS_MAX");
+            if (cap_env)
+                while (log2s > 0 && (1ull << log2s) > std::strtoull(cap_env, nullptr, 10)) log2s--;
+        };
+        plan();
         if (count) {
-            // a device short of memory (another process, a smaller part) gets smaller chunks, down to one frame,
-            // instead of a failed draw
-            while ((rc = ensure(r->samples, (size_t)chunk * frame_floats)) == RT_ERR_ALLOC && chunk > 1u) {
+            for (;;) {
+                rc = ensure(r->ring, ((size_t)chunk << log2s) * 64u);
+                if (!rc) rc = ensure(r->ring_ctl, 2ull << log2s);
+                if (rc != RT_ERR_ALLOC || budget <= (64u << 10)) break;
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
-                chunk = (chunk + 1u) / 2u;
+                budget /= 2u;
+                plan();
             }
             if (rc) return rc;
         }
-        P.samples = r->samples.ptr;
+        P.ring = r->ring.ptr;
+        P.ring_log2 = log2s;
+        P.ring_bytes = (uint32_t)(((size_t)chunk << log2s) * 1024u);
+        P.ring_done = r->ring_ctl.ptr;
+        P.ring_folds = r->ring_ctl.ptr + (1u << log2s);
         P.queue = r->counter.ptr + 15;
+        r->ring_slots = 1u << log2s;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
         for (uint32_t done = 0; done < count; done += chunk) {
             P.nframes = std::min(chunk, count - done);
@@ -487,17 +509,17 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.suspend_below = split ? r->params.suspend_below : 0u;
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
-            P.njobs = (unsigned long long)P.tiles_w * P.tiles_h * P.nchunks;
+            P.njobs = (unsigned long long)ntiles * P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
-            rc = trace_events(r, launches / 2u);
+            HIP_TRY(hipMemsetAsync(P.ring_done, 0, (2ull << log2s) * sizeof(uint32_t), r->stream));
+            rc = trace_events(r, launches);
             if (rc) return rc;
-            HIP_TRY(hipEventRecord(r->ev_trace[launches], r->stream));
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * launches], r->stream));
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
-            HIP_TRY(hipEventRecord(r->ev_trace[launches + 1], r->stream));
-            HIP_TRY(hrt_launch_accumulate(P, r->stream));
-            launches += 2;
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * launches + 1], r->stream));
+            launches++;
         }
-        r->trace_pairs = launches / 2u;
+        r->trace_pairs = launches;
     } else {
         const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
@@ -517,6 +539,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.launches = launches;
     r->stats.local_rows = P.nrows;
     std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
+    if (schedule == RT_SCHEDULE_QUEUE && count)
+        r->stats.ring_bytes = (uint64_t)P.ring_bytes + 8ull * r->ring_slots;
     r->timing_pending = true;
     return RT_OK;
 }
@@ -566,7 +590,7 @@ int rt_device_count(void) {
 }
 
 const char* rt_build_info(void) {
-    return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_trace_split, k_trace_split_tris, k_trace, k_accumulate, "
+    return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_trace_split, k_trace_split_tris, k_trace, "
            "k_render";
 }
 
@@ -592,7 +616,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.schedule = RT_SCHEDULE_AUTO;
     // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one chunk (one k_trace launch per draw, one launch
     // tail instead of six): C3 25.9 -> 26.1 Grays/s over 4 GiB
-    r->params.queue_budget_mb = 32768;
+    r->params.queue_budget_mb = 768;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
     r->params.job_frames = 0;  // per kernel (rt_draw_frames)

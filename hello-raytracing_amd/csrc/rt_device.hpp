@@ -132,8 +132,13 @@ struct KParams {
     const MatDev* mats;
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
     unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
-    // sample-queue schedule (k_trace / k_accumulate)
-    float* samples;               // nframes x (tiles_w * tiles_h) x 64 px x 3 colours, frame- then tile-major
+    // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris): the fold ring. A tile's samples go to
+    // ring slot tile % ring_slots; the wave that completes the tile's last job folds them into the image.
+    float4* ring;                 // ring_slots x nframes x 64 px colour (r, g, b, unused)
+    uint32_t* ring_done;          // [slot]: jobs completed in the slot (cumulative over the tiles it holds)
+    uint32_t* ring_folds;         // [slot]: tiles folded out of the slot (the generation allowed to write)
+    uint32_t ring_log2;           // ring_slots = 1 << ring_log2
+    uint32_t ring_bytes;          // size of `ring` (buffer-descriptor range)
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows

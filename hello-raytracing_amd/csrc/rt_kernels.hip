@@ -876,6 +876,231 @@ __device__ __forceinline__ LaneLists lane_lists() {
     return L;
 }
 
+// ---- The fold ring (sample queue) ----
+// A job is one 8x8 tile x job_frames frames, taken by ONE wave from the queue; a tile's jobs are dealt one
+// after another (tile-major), so they run at once on neighbouring waves. Each sample's colour goes to the
+// tile's ring slot (slot = tile % ring_slots, frame-major, 16 B per pixel) as a write-through (sc1) store.
+// A wave tracks its jobs (WaveJobs); when every sample of one has been stored it drains its stores
+// (s_waitcnt vmcnt(0)) and adds 1 to the slot's job count (agent-scope atomic). The wave whose add completes
+// the tile folds the slot into the image, frame by frame in order (the expression of k_render; sc1 loads
+// behind an agent acquire), then releases the slot to the tile ring_slots further on, whose jobs wait for
+// it. Memory is O(tiles in flight) instead of O(frames x pixels), and there is no separate fold pass.
+// Hand-off form: MI355X_MICROARCH.md § visibility, row 1 of the sc1 table (the storing unit is the wave:
+// all a job's samples are stored by the wave that dealt it).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc() {
+    const KPtr K = kargs();
+    return __builtin_amdgcn_make_buffer_rsrc((void*)K->ring, (short)0, (int)K->ring_bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void ring_store(uint32_t pix, uint32_t fl, const f3 c) {
+    const KPtr K = kargs();
+    const uint32_t slot = (pix >> 6) & ((1u << K->ring_log2) - 1u);
+    const uint32_t off = (((slot * K->nframes + fl) << 6) | (pix & 63u)) << 4;
+    const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16 /* sc1: write-through */);
+}
+
+// Folds tile `tile`'s slot (all P.nframes frames, in order) into the image; the whole wave, lane = pixel.
+__device__ __forceinline__ void fold_tile(uint32_t tile) {
+    const KPtr K = kargs();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t slot = tile & ((1u << K->ring_log2) - 1u);
+    const uint32_t x = (tile % K->tiles_w) * 8u + (lane & 7u);
+    const uint32_t kr = (tile / K->tiles_w) * 8u + (lane >> 3);
+    const bool ok = x < K->W && kr < K->nrows;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    float* px = K->image + ((size_t)(ok ? kr : 0u) * K->W + (ok ? x : 0u)) * 3u;
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    if (ok) {
+        a0 = px[0];
+        a1 = px[1];
+        a2 = px[2];
+    }
+    const __amdgpu_buffer_rsrc_t rs = ring_rsrc();
+    const uint32_t nf = K->nframes, frame0 = K->frame0;
+    const float cap = K->ema_cap;
+    uint32_t off = ((slot * nf) << 10) | (lane << 4);
+    constexpr uint32_t U = 2;
+    uint32_t f = 0;
+    for (; f + U <= nf; f += U) {
+        u32x4 c[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) c[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + (u << 10)), 0, 16);
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const float w = 1.0f / (fmin_ieee((float)(frame0 + f + u), cap) + 1.0f);
+            const float omw = 1.0f - w;
+            a0 = a0 * omw + (0.0f + __uint_as_float(c[u].x)) * w;
+            a1 = a1 * omw + (0.0f + __uint_as_float(c[u].y)) * w;
+            a2 = a2 * omw + (0.0f + __uint_as_float(c[u].z)) * w;
+        }
+        off += U << 10;
+    }
+    for (; f < nf; f++, off += 1u << 10) {
+        const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
+        const float w = 1.0f / (fmin_ieee((float)(frame0 + f), cap) + 1.0f);
+        const float omw = 1.0f - w;
+        a0 = a0 * omw + (0.0f + __uint_as_float(c.x)) * w;
+        a1 = a1 * omw + (0.0f + __uint_as_float(c.y)) * w;
+        a2 = a2 * omw + (0.0f + __uint_as_float(c.z)) * w;
+    }
+    if (ok) {
+        px[0] = a0;
+        px[1] = a1;
+        px[2] = a2;
+    }
+    // every load of the slot has returned (its values are folded); then the slot passes to the next tile
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(K->ring_folds + slot, (tile >> K->ring_log2) + 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// The wave's jobs whose samples are not all stored yet: the current one (being dealt, or waiting for its ring
+// slot) and up to WJ_NE - 1 older ones with samples still in flight (a 50-bounce path can outlive several
+// jobs of its wave). Kept in LDS, one block of words per wave (every lane reads and writes the same values),
+// not in registers: the walk kernels have no SGPRs to spare.
+constexpr uint32_t WJ_NE = 4;
+enum : uint32_t { WJ_TILE = 0, WJ_F0 = WJ_NE, WJ_LIVE = 2 * WJ_NE, WJ_FLAGS = 3 * WJ_NE, WJ_STAT = 3 * WJ_NE + 1 };
+// flags: busy bit per entry (bits 0..WJ_NE-1), the current entry (bits 8-9), dealing, waiting
+enum : uint32_t { WJ_BUSY = (1u << WJ_NE) - 1u, WJ_CUR_SHIFT = 8, WJ_DEALING = 1u << 12, WJ_WAITING = 1u << 13 };
+struct WaveJobs {
+    uint32_t* w;  // this wave's words
+    __device__ uint32_t get(uint32_t i) const { return uniform(w[i]); }
+    __device__ void set(uint32_t i, uint32_t v) const { w[i] = v; }
+    __device__ bool dealing() const { return (get(WJ_FLAGS) & WJ_DEALING) != 0u; }
+    __device__ bool idle() const { return (get(WJ_FLAGS) & WJ_BUSY) == 0u; }
+};
+
+#ifdef HRT_RINGSTAT
+// diagnostic build: per-wave ring statistics (stall rounds: every entry busy; slot-wait rounds; folds; fold
+// cycles / 16), summed into counter[5..8] at wave exit
+#define WJ_WORDS (WJ_STAT + 4u)
+#define RINGSTAT_ADD(J, i, v) (J).set(WJ_STAT + (i), (J).get(WJ_STAT + (i)) + (uint32_t)(v))
+#else
+#define WJ_WORDS (WJ_STAT)
+#define RINGSTAT_ADD(J, i, v) ((void)0)
+#endif
+
+__device__ __forceinline__ WaveJobs wave_jobs(uint32_t* lds) {
+    WaveJobs J{lds + (threadIdx.x >> 6) * WJ_WORDS};
+    if ((threadIdx.x & 63u) < WJ_WORDS) J.w[threadIdx.x & 63u] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return J;
+}
+
+// One job of the wave is complete (every sample stored): count it in its slot. true: it completed the tile, which
+// the wave must now fold.
+__device__ __forceinline__ bool job_complete(uint32_t tile, uint32_t lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores have reached memory
+    const KPtr K = kargs();
+    const uint32_t slot = tile & ((1u << K->ring_log2) - 1u);
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(K->ring_done + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = uniform(__shfl(old, 0));
+    return old + 1u == ((tile >> K->ring_log2) + 1u) * K->nchunks;
+}
+
+// The current job is dealt out (it completes in job_account once nothing of it is in flight).
+__device__ __forceinline__ void job_close(const WaveJobs& J, uint32_t /*lane*/) {
+    J.set(WJ_FLAGS, J.get(WJ_FLAGS) & ~WJ_DEALING);
+}
+
+// Makes a job current and dealable: fetch one into a free entry and wait for its slot.
+// false: nothing to deal now (queue drained -> `drained`; every entry still in flight; slot still folding).
+__device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bool& drained, uint32_t& job_tile,
+                                            uint32_t& job_f0, uint32_t& job_nf) {
+    const KPtr K = kargs();
+    uint32_t flags = J.get(WJ_FLAGS);
+    if (!(flags & WJ_WAITING)) {
+        if ((flags & WJ_BUSY) == WJ_BUSY) {  // every entry still has samples in flight
+            RINGSTAT_ADD(J, 0, 1);
+            return false;
+        }
+        const uint32_t e = (uint32_t)__builtin_ctz(~flags & WJ_BUSY);
+        uint32_t j = 0;
+        if (lane == 0) j = (uint32_t)atomicAdd(K->queue, 1ull);
+        j = uniform(__shfl(j, 0));
+        if (j >= K->njobs) {
+            drained = true;
+            return false;
+        }
+        J.set(WJ_TILE + e, j / K->nchunks);
+        J.set(WJ_F0 + e, (j % K->nchunks) * K->job_frames);
+        J.set(WJ_LIVE + e, 0u);
+        flags = (flags & ~(3u << WJ_CUR_SHIFT)) | (1u << e) | (e << WJ_CUR_SHIFT) | WJ_WAITING;
+        J.set(WJ_FLAGS, flags);
+    }
+    const uint32_t cur = (flags >> WJ_CUR_SHIFT) & 3u;
+    const uint32_t t = J.get(WJ_TILE + cur);
+    uint32_t folds = 0;
+    if (lane == 0)
+        folds = __hip_atomic_load(K->ring_folds + (t & ((1u << K->ring_log2) - 1u)), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    folds = uniform(__shfl(folds, 0));
+    if (folds < (t >> K->ring_log2)) {  // the slot's previous tile is not folded yet
+        RINGSTAT_ADD(J, 1, 1);
+        return false;
+    }
+    J.set(WJ_FLAGS, (flags & ~WJ_WAITING) | WJ_DEALING);
+    job_tile = t;
+    job_f0 = J.get(WJ_F0 + cur);
+    job_nf = min(K->job_frames, K->nframes - job_f0);
+    return true;
+}
+
+// Samples just dealt from the current job (lanes that took one).
+__device__ __forceinline__ void job_dealt(const WaveJobs& J, uint32_t n) {
+    if (n == 0u) return;
+    const uint32_t i = WJ_LIVE + ((J.get(WJ_FLAGS) >> WJ_CUR_SHIFT) & 3u);
+    J.set(i, J.get(i) + n);
+}
+
+// End of a round: lanes whose sample finished (`fin`, colour stored) are counted off their jobs (the busy entry
+// whose tile and frames hold the sample); jobs neither current nor with anything in flight complete, and a job
+// that completes its tile folds it.
+__device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_t pix, uint32_t fl, uint32_t lane) {
+    const unsigned long long any = __ballot(fin);
+    if (any != 0ull) {
+        const KPtr K = kargs();
+        const uint32_t busy = J.get(WJ_FLAGS) & WJ_BUSY;
+        uint32_t idx = 0;
+#pragma unroll
+        for (uint32_t e = 1; e < WJ_NE; e++)
+            if (((busy >> e) & 1u) && (pix >> 6) == J.get(WJ_TILE + e) && fl - J.get(WJ_F0 + e) < K->job_frames)
+                idx = e;
+#pragma unroll
+        for (uint32_t e = 0; e < WJ_NE; e++) {
+            const uint32_t n = (uint32_t)__popcll(__ballot(fin && idx == e));
+            if (n) J.set(WJ_LIVE + e, J.get(WJ_LIVE + e) - n);
+        }
+    }
+#pragma nounroll
+    for (uint32_t e = 0; e < WJ_NE; e++) {
+        const uint32_t flags = J.get(WJ_FLAGS);
+        const bool current = ((flags >> WJ_CUR_SHIFT) & 3u) == e && (flags & (WJ_DEALING | WJ_WAITING));
+        if (((flags >> e) & 1u) && J.get(WJ_LIVE + e) == 0u && !current) {
+            J.set(WJ_FLAGS, flags & ~(1u << e));
+            const uint32_t t = J.get(WJ_TILE + e);
+            if (job_complete(t, lane)) {
+#ifdef HRT_RINGSTAT
+                const unsigned long long t0 = __builtin_readcyclecounter();
+#endif
+                fold_tile(t);
+#ifdef HRT_RINGSTAT
+                RINGSTAT_ADD(J, 2, 1);
+                RINGSTAT_ADD(J, 3, (__builtin_readcyclecounter() - t0) >> 4);
+#endif
+            }
+        }
+    }
+}
+
 // Refill with primary rays by frame block (k_trace with the simple sphere scan): when the wave's block
 // (one frame of its job's 8x8 tile) is used up, every lane computes the primary ray of its own pixel for
 // the next frame at once (all lanes busy), and lanes that need a sample fetch one from the block's owner
@@ -889,7 +1114,7 @@ struct BlockQueue {
 
 // Free lanes (!have) take the next samples; sets drained once the job queue is empty.
 template <int MODE>
-__device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bool& drained, uint32_t lane,
+__device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, const WaveJobs& J, bool& drained, uint32_t lane,
                                              unsigned long long below, bool& have, Ray& ray, f3& att,
                                              float& sky_t, uint32_t& s, uint32_t& bounce, uint32_t& pix,
                                              uint32_t& fl) {
@@ -897,20 +1122,10 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bo
     unsigned long long m = __ballot(need);
     while (m != 0ull) {
         if (B.blk_next == 64u) {
-            if (B.blk_f + 1u < B.job_nf) {
+            if (J.dealing()) {
                 B.blk_f++;
             } else {
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(P.queue, 1ull);
-                j = __shfl(j, 0);
-                if (j >= P.njobs) {
-                    drained = true;
-                    break;
-                }
-                const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                B.job_tile = (uint32_t)(j / P.nchunks);
-                B.job_f0 = chunk * P.job_frames;
-                B.job_nf = min(P.job_frames, P.nframes - B.job_f0);
+                if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
             }
             B.blk_next = 0;
@@ -930,6 +1145,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bo
         const float ox = __shfl(B.pr_o.x, src), oy = __shfl(B.pr_o.y, src), oz = __shfl(B.pr_o.z, src);
         const float dx = __shfl(B.pr_d.x, src), dy = __shfl(B.pr_d.y, src), dz = __shfl(B.pr_d.z, src);
         const uint32_t ss = __shfl(B.pr_s, src), ok = __shfl(B.pr_ok, src);
+        bool took = false;
         if (need && rank < avail) {
             need = false;
             if (ok) {
@@ -942,9 +1158,12 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, bo
                 att = mk(1.0f, 1.0f, 1.0f);
                 bounce = 0;
                 have = true;
+                took = true;
             }
         }
+        job_dealt(J, (uint32_t)__popcll(__ballot(took)));
         B.blk_next += min((uint32_t)__popcll(m), avail);
+        if (B.blk_next == 64u && B.blk_f + 1u >= B.job_nf) job_close(J, lane);
         m = __ballot(need);
     }
 }
@@ -1107,10 +1326,10 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // next job as soon as the current one has no samples left, while older samples are still in flight.
 // Lanes therefore never idle until the queue is empty, a wave's lanes stay inside one tile (ray
 // coherence: an incoherent sample queue measured 2.65x slower on C3), and one tile's frames are
-// spread over many waves. Each sample's colour goes to a frame-major, tile-major buffer (a tile's frame is
-// 768 contiguous bytes, so colour stores fill whole cache lines); k_accumulate then folds
-// the colours into the image in frame order per pixel with the reference's mix
-// (shader_sphere.wgsl:264-271), so the image is bit-identical to k_render's and to count x rt_draw.
+// spread over many waves. Each sample's colour goes to its tile's slot of the fold ring, and the wave that
+// completes a tile's last job folds the slot into the image in frame order per pixel with the reference's
+// mix (shader_sphere.wgsl:264-271; fold_tile), so the image is bit-identical to k_render's and to
+// count x rt_draw.
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
 // (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
@@ -1126,8 +1345,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     const unsigned long long below = (1ull << lane) - 1ull;
 
     // wave-uniform job state
-    uint32_t job_tile = 0, job_f0 = 0, job_next = 0, job_total = 0;
+    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, job_next = 0, job_total = 0;
     BlockQueue BQ;  // frame-block refill (simple sphere scan only)
+    __shared__ uint32_t wjobs[4 * WJ_WORDS];
+    const WaveJobs J = wave_jobs(wjobs);
     bool drained = false;
     // lane state
     Ray ray;
@@ -1151,29 +1372,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         constexpr bool BLOCK_REFILL = MODE == MODE_SPHERE && SCAN == SCAN_SIMPLE;
         bool need = !have && !drained;
         if constexpr (BLOCK_REFILL) {
-            refill_block<MODE>(P, BQ, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
+            refill_block<MODE>(P, BQ, J, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
             need = false;
         }
         unsigned long long m = __ballot(need);
         while (m != 0ull) {
-            if (job_next == job_total) {
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(P.queue, 1ull);
-                j = __shfl(j, 0);
-                if (j >= P.njobs) {
-                    drained = true;
-                    break;
-                }
+            if (!J.dealing()) {
                 // tile-major job order: one tile's frame chunks are handed out together and run on
                 // neighbouring waves at once, so an expensive tile finishes early instead of trailing
-                const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                job_tile = (uint32_t)(j / P.nchunks);
-                job_f0 = chunk * P.job_frames;
-                job_total = 64u * min(P.job_frames, P.nframes - job_f0);
+                if (!job_acquire(J, lane, drained, job_tile, job_f0, job_nf)) break;
+                job_total = 64u * job_nf;
                 job_next = 0;
             }
             const uint32_t avail = job_total - job_next;
             const uint32_t rank = (uint32_t)__popcll(m & below);
+            bool took_ok = false;
             if (need && rank < avail) {
                 const uint32_t sid = job_next + rank;
                 const uint32_t l = sid & 63u;
@@ -1189,20 +1402,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                     att = mk(1.0f, 1.0f, 1.0f);
                     bounce = 0;
                     have = true;
+                    took_ok = true;
                 }
             }
+            job_dealt(J, (uint32_t)__popcll(__ballot(took_ok)));
             const uint32_t took = min((uint32_t)__popcll(m), avail);
             job_next += took;
+            if (job_next == job_total) job_close(J, lane);
             m = __ballot(need);
         }
 #ifdef HRT_STAMPS
         st_tb = hrt_stamp();
         if (have) st_gen += st_tb - st_ta;
 #endif
-        if (drained && __ballot(have) == 0ull) break;
-        if (!have) continue;
-        bool done = true;
-        if (bounce < P.bounces) {
+        if (__ballot(have) == 0ull) {
+            if (drained && J.idle()) break;
+            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+        }
+        bool fin = false;
+        bool done = have;
+        if (have && bounce < P.bounces) {
             Hit h;
 #ifdef HRT_STAMPS
             const uint32_t boxes0 = tally.boxes;
@@ -1227,20 +1446,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             }
         }
         if (done) {
-            // trace() epilogue (:241-242): the sample colour, folded in by k_accumulate
+            // trace() epilogue (:241-242): the sample colour, to the fold ring
             const float u = 1.0f - sky_t;
             const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
             const f3 c = att * sky;
-            const KPtr K = kargs();
-            float* o = K->samples + ((size_t)fl * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
-            o[0] = c.x;
-            o[1] = c.y;
-            o[2] = c.z;
+            ring_store(pix, fl, c);
             have = false;
+            fin = true;
         }
 #ifdef HRT_STAMPS
         st_shade += hrt_stamp() - st_tb;
 #endif
+        job_account(J, fin, pix, fl, lane);
     }
 #ifdef HRT_STAMPS
     {
@@ -1265,6 +1482,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         }
     }
 #endif
+#ifdef HRT_RINGSTAT
+    if (lane == 0)
+        for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
+#endif
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
@@ -1287,7 +1508,7 @@ struct BlockState {
 };
 
 template <int MODE>
-__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, float4* blk, bool& drained,
+__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float4* blk, bool& drained,
                                                  uint32_t lane, unsigned long long below, bool& have,
                                                  uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
                                                  uint32_t& bounce, uint32_t& pix, uint32_t& fl) {
@@ -1296,20 +1517,10 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
     while (m != 0ull) {
         if (B.blk_next == 64u) {
             const KPtr K = kargs();  // queue and camera constants: loaded here, not held in SGPRs
-            if (B.blk_f + 1u < B.job_nf) {
+            if (J.dealing()) {
                 B.blk_f++;
             } else {
-                unsigned long long j = 0;
-                if (lane == 0) j = atomicAdd(K->queue, 1ull);
-                j = __shfl(j, 0);
-                if (j >= K->njobs) {
-                    drained = true;
-                    break;
-                }
-                const uint32_t chunk = (uint32_t)(j % K->nchunks);
-                B.job_tile = (uint32_t)(j / K->nchunks);
-                B.job_f0 = chunk * K->job_frames;
-                B.job_nf = min(K->job_frames, K->nframes - B.job_f0);
+                if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
             }
             B.blk_next = 0;
@@ -1333,6 +1544,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
         const uint32_t src = (B.blk_next + rank) & 63u;
         const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + src)];
         const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + src) + 1];
+        bool took = false;
         if (need && rank < avail) {
             need = false;
             if (__float_as_uint(b1.w)) {
@@ -1346,9 +1558,12 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 bounce = 0;
                 have = true;
                 qs = 0;
+                took = true;
             }
         }
+        job_dealt(J, (uint32_t)__popcll(__ballot(took)));
         B.blk_next += min((uint32_t)__popcll(m), avail);
+        if (B.blk_next == 64u && B.blk_f + 1u >= B.job_nf) job_close(J, lane);
         m = __ballot(need);
     }
 }
@@ -1399,25 +1614,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     // once (all lanes busy) into the wave's slice of `blk`, and lanes that need a sample read theirs from
     // it, instead of each freed lane computing its own with a few lanes active.
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+    __shared__ uint32_t wjobs[4 * WJ_WORDS];
+    const WaveJobs J = wave_jobs(wjobs);
     while (true) {
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
         while (m != 0ull) {
             if (blk_next == 64u) {
-                if (blk_f + 1u < job_nf) {
+                if (J.dealing()) {
                     blk_f++;
                 } else {
-                    unsigned long long j = 0;
-                    if (lane == 0) j = atomicAdd(P.queue, 1ull);
-                    j = __shfl(j, 0);
-                    if (j >= P.njobs) {
-                        drained = true;
-                        break;
-                    }
-                    const uint32_t chunk = (uint32_t)(j % P.nchunks);
-                    job_tile = (uint32_t)(j / P.nchunks);
-                    job_f0 = chunk * P.job_frames;
-                    job_nf = min(P.job_frames, P.nframes - job_f0);
+                    if (!job_acquire(J, lane, drained, job_tile, job_f0, job_nf)) break;
                     blk_f = 0;
                 }
                 blk_next = 0;
@@ -1443,6 +1650,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src) + 1];
             const float ox = b0.x, oy = b0.y, oz = b0.z, dx = b0.w, dy = b1.x, dz = b1.y;
             const uint32_t ss = __float_as_uint(b1.z), ok = __float_as_uint(b1.w);
+            bool took = false;
             if (need && rank < avail) {
                 need = false;
                 if (ok) {
@@ -1456,12 +1664,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     bounce = 0;
                     have = true;
                     qs = 0;
+                    took = true;
                 }
             }
+            job_dealt(J, (uint32_t)__popcll(__ballot(took)));
             blk_next += min((uint32_t)__popcll(m), avail);
+            if (blk_next == 64u && blk_f + 1u >= job_nf) job_close(J, lane);
             m = __ballot(need);
         }
-        if (drained && __ballot(have) == 0ull) break;
+        if (__ballot(have) == 0ull) {
+            if (drained && J.idle()) break;
+            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+        }
+        bool fin = false;
 #ifdef HRT_STAMPS
         if (lane == 0) tally.rounds++;
 #endif
@@ -1503,14 +1718,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                float* o = P.samples + ((size_t)fl * P.tiles_w * P.tiles_h * 64u + pix) * 3u;
-                o[0] = c.x;
-                o[1] = c.y;
-                o[2] = c.z;
+                ring_store(pix, fl, c);
                 have = false;
+                fin = true;
             }
             qs = 0u;
         }
+        job_account(J, fin, pix, fl, lane);
     }
 #ifdef HRT_STAMPS
     {
@@ -1524,6 +1738,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         if (lane == 0)
             for (int c = 0; c < 7; c++) atomicAdd(P.counter + 5 + c, v[c]);
     }
+#endif
+#ifdef HRT_RINGSTAT
+    if (lane == 0)
+        for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
 #endif
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
@@ -1565,6 +1783,8 @@ k_trace_split_tris(const KParams P) {
 
     __shared__ float4 blk[2 * 256];  // the wave's frame block (refill_block_lds)
     BlockState B;
+    __shared__ uint32_t wjobs[4 * WJ_WORDS];
+    const WaveJobs J = wave_jobs(wjobs);
     bool drained = false;
     Ray ray;
     f3 att = mk(1.0f, 1.0f, 1.0f);
@@ -1576,8 +1796,12 @@ k_trace_split_tris(const KParams P) {
     int bi = -1;  // sphere winner slot
     HeapWalk W;
     while (true) {
-        refill_block_lds<MODE>(P, B, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
-        if (drained && __ballot(have) == 0ull) break;
+        refill_block_lds<MODE>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
+        if (__ballot(have) == 0ull) {
+            if (drained && J.idle()) break;
+            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+        }
+        bool fin = false;
         if (have && qs == 0u) {
             if (bounce >= P.bounces) {
                 qs = 5u;  // bounce cap 0: the sample is the sky colour
@@ -1618,16 +1842,18 @@ k_trace_split_tris(const KParams P) {
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                const KPtr K = kargs();
-                float* o = K->samples + ((size_t)fl * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
-                o[0] = c.x;
-                o[1] = c.y;
-                o[2] = c.z;
+                ring_store(pix, fl, c);
                 have = false;
+                fin = true;
             }
             qs = 0u;
         }
+        job_account(J, fin, pix, fl, lane);
     }
+#ifdef HRT_RINGSTAT
+    if (lane == 0)
+        for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
+#endif
     unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
@@ -1639,33 +1865,6 @@ k_trace_split_tris(const KParams P) {
         for (int c = 0; c < 5; c++)
             if (sums[c]) atomicAdd(P.counter + c, sums[c]);
     }
-}
-
-// Folds P.nframes sample colours per pixel into the image, in frame order, with the same expression
-// k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per tile-padded pixel, in the buffer's
-// tile-major order, so the frame-major colour reads are contiguous across the wave.
-__global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
-    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
-    const size_t q = (size_t)blockIdx.x * 256u + threadIdx.x;
-    if (q >= npad) return;
-    const uint32_t tile = (uint32_t)(q >> 6), l = (uint32_t)(q & 63u);
-    const uint32_t x = (tile % P.tiles_w) * 8u + (l & 7u);
-    const uint32_t kr = (tile / P.tiles_w) * 8u + (l >> 3);
-    if (x >= P.W || kr >= P.nrows) return;
-    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
-    float acc0 = px[0], acc1 = px[1], acc2 = px[2];
-    const float* c = P.samples + q * 3u;
-    for (uint32_t f = 0; f < P.nframes; f++, c += npad * 3u) {
-        const float fc = (float)(P.frame0 + f);
-        const float w = 1.0f / (fmin_ieee(fc, P.ema_cap) + 1.0f);
-        const float omw = 1.0f - w;
-        acc0 = acc0 * omw + (0.0f + c[0]) * w;
-        acc1 = acc1 * omw + (0.0f + c[1]) * w;
-        acc2 = acc2 * omw + (0.0f + c[2]) * w;
-    }
-    px[0] = acc0;
-    px[1] = acc1;
-    px[2] = acc2;
 }
 
 // Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE
@@ -1781,14 +1980,6 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
         return P.tri_bvh ? launch_trace_mode<MODE_MIXED, true>(variant, P, stream)
                          : launch_trace_mode<MODE_MIXED, false>(variant, P, stream);
     }
-}
-
-// Sample queue, part 2: fold the chunk's colours into the image in frame order.
-hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
-    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
-    if (npad == 0 || P.nframes == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npad + 255u) / 256u)), dim3(256), 0, stream, P);
-    return hipGetLastError();
 }
 
 // Host-side launcher of the tiles schedule (called from renderer.cpp; no HIP types in the C-ABI).

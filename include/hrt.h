@@ -68,7 +68,7 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue colour buffer budget in MiB (frames per chunk); 32768  */
+    uint32_t queue_budget_mb;  /* sample-queue fold-ring budget in MiB (slots, frames per launch); 768 */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 0 = per
                                   kernel: 32 with the suspendable walks, 16 for the linear sphere scans */
     uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
@@ -106,6 +106,8 @@ typedef struct rt_stats {
                               0 = every query ran to completion (k_trace, k_render)                    */
     char kernel[64];       /* the ray-tracing kernel the last draw ran, as rocprofv3 names it without
                               "void " and the argument list, e.g. "k_trace_split<true>"                 */
+    uint64_t ring_bytes;   /* device memory of the sample queue's fold ring (slots x frames x 64 px x 16 B,
+                              plus 8 B of control per slot) in the last draw; 0 for the tiles schedule   */
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

@@ -148,7 +148,7 @@ def config_c1() -> SceneDef:
                     min_sphere_slots=0)
 
 
-def config_c2() -> SceneDef:
+def config_c2(width: int = 1280, height: int = 720, frames: int = 256) -> SceneDef:
     """C2: ground + Lambertian / Metal(0.1) / Dielectric(1.5), 1280x720, 256 spp, 50 bounces."""
     cam = Camera.new(Vec3(0.0, 0.2, 1.5), Vec3(0.0, 0.1, -3.0), 2.2, 0.05, PI * f32(0.3))
     sp = hrt.spheres_array([
@@ -157,7 +157,7 @@ def config_c2() -> SceneDef:
         Sphere.new_metal(Vec3(1.0, 0.0, -1.0), 0.5, Vec3(0.8, 0.6, 0.2), 0.1),
         Sphere.new_dielectric(Vec3(-1.0, 0.0, -1.0), 0.5, 1.5),
     ])
-    return SceneDef("C2-three-spheres", hrt.RT_MODE_SPHERE, 1280, 720, cam, sp, frames=256, bounces=50,
+    return SceneDef("C2-three-spheres", hrt.RT_MODE_SPHERE, width, height, cam, sp, frames=frames, bounces=50,
                     min_sphere_slots=0)
 
 

@@ -154,17 +154,18 @@ def test_auto_schedule_by_draw_size():
 
 
 def test_sample_queue_chunks_and_tris_mode():
-    """Frame chunks bounded by the colour-buffer budget (1 and 2 frames per chunk at 320x240) and the
-    triangle program under the queue schedule."""
+    """Launches bounded by the fold-ring budget (1 MiB at 320x240: 256 slots of 4 frames, 1200 tiles sharing
+    them: two launches; 2 MiB: one), and the triangle program under the queue schedule."""
     sd = scenes.golden_scene("metal_materials", 320, 240)
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
     ref.draw_frames(5, 1000, 10)
-    for mb in (1, 2):
+    for mb, launches in ((1, 2), (2, 1)):
         r = scenes.make_renderer(sd)
         r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb)
         r.draw_frames(5, 1000, 10)
-        assert r.stats().launches == 2 * ((5 + mb - 1) // mb)
+        st = r.stats()
+        assert st.launches == launches and st.ring_bytes == 256 * min(5, 4 * mb) * 1024 + 8 * 256, (st.launches, st.ring_bytes)
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     scene = hrt.SceneTris.new_suzane(96, 72)
     scene.init()
@@ -180,34 +181,58 @@ def test_sample_queue_chunks_and_tris_mode():
     assert_parity(imgs[1], ref_img, "suzane tris, queue schedule")
 
 
-def test_sample_buffer_allocation_failure_halves_the_chunk():
-    """A colour-buffer allocation the device refuses (fault injection: every allocation above 100 MiB fails
-    in a subprocess with HRT_FAIL_ALLOC_ABOVE_MB=100): the renderer halves the chunk until one fits and the
-    draw completes, bit-identical to the default single-chunk draw."""
+def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, out_name: str):
+    """Renders `scene_expr` (a scenes.* SceneDef) under the queue schedule in a child process with extra
+    environment (the fault-injection and slot-cap knobs are read once per process); returns (image, stats)."""
+    import json
+    import os
     import subprocess
     import sys
-
-    code = ("import sys; sys.path[:0] = ['hello-raytracing_amd', 'tests']; import numpy as np, scenes, hrt\n"
-            "sd = scenes.golden_scene('metal_materials', 512, 512); r = scenes.make_renderer(sd)\n"
-            "r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE); r.draw_frames(40, 1000, 10)\n"
-            "np.save(sys.argv[1], r.read_image()); print(r.stats().launches)\n")
     from pathlib import Path
+
+    code = ("import sys, json; sys.path[:0] = ['hello-raytracing_amd', 'tests']; import numpy as np, scenes, hrt\n"
+            f"sd = {scene_expr}; r = scenes.make_renderer(sd)\n"
+            f"r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE); r.draw_frames({frames}, 1000, 10)\n"
+            "np.save(sys.argv[1], r.read_image()); st = r.stats()\n"
+            "print(json.dumps({'launches': st.launches, 'ring_bytes': st.ring_bytes, 'queries': st.queries}))\n")
     root = Path(__file__).resolve().parents[1]
     out = root / "tests" / "output"
     out.mkdir(exist_ok=True)
-    import os
-    env = dict(os.environ, HRT_FAIL_ALLOC_ABOVE_MB="100")
-    p = subprocess.run([sys.executable, "-c", code, str(out / "alloc_small.npy")], cwd=root, env=env,
+    p = subprocess.run([sys.executable, "-c", code, str(out / out_name)], cwd=root, env=dict(os.environ, **env_extra),
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert int(p.stdout.split()[-1]) >= 4  # 40 frames x 3 MiB do not fit in 100 MiB: at least two chunks
+    return np.load(out / out_name), json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_fold_ring_allocation_failure_halves_the_budget():
+    """A fold-ring allocation the device refuses (fault injection: every allocation above 100 MiB fails in a
+    subprocess with HRT_FAIL_ALLOC_ABOVE_MB=100): the renderer halves its budget (fewer slots) until the ring
+    fits and the draw completes, bit-identical to the default draw."""
+    small, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"},
+                                            "scenes.golden_scene('metal_materials', 512, 512)", 40, "alloc_small.npy")
+    assert 0 < st["ring_bytes"] <= 100 << 20, st  # 4096 tiles x 40 KB = 160 MiB do not fit: 2048 slots
     sd = scenes.golden_scene("metal_materials", 512, 512)
     r = scenes.make_renderer(sd)
     r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE)
     r.draw_frames(40, 1000, 10)
-    assert r.stats().launches == 2
-    small = np.load(out / "alloc_small.npy")
+    assert r.stats().launches == 1 and r.stats().ring_bytes > 100 << 20
     np.testing.assert_array_equal(small.view(np.uint32), r.read_image().view(np.uint32))
+
+
+@pytest.mark.parametrize("slots", [1, 2, 8])
+def test_fold_ring_slot_reuse_bit_identical(slots):
+    """Very few fold-ring slots (HRT_RING_SLOTS_MAX): nearly every tile waits for the fold of the tile that
+    held its slot before it. C3 (k_trace_split) and C4 (k_trace_split_tris) at 160x96, 64 frames (two jobs per
+    tile), and C2 (k_trace): images bit-identical to the tiles schedule, same ray counts."""
+    for expr in ("scenes.config_c3(160, 96, 64)", "scenes.config_c4(160, 96, 64)", "scenes.config_c2(160, 96, 64)"):
+        img, st = _queue_render_in_subprocess({"HRT_RING_SLOTS_MAX": str(slots)}, expr, 64, f"ring_{slots}.npy")
+        assert st["ring_bytes"] == slots * 64 * 1024 + 8 * slots, st
+        sd = eval(expr)
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_TILES)
+        r.draw_frames(64, 1000, 10)
+        np.testing.assert_array_equal(img.view(np.uint32), r.read_image().view(np.uint32), err_msg=expr)
+        assert st["queries"] == r.stats().queries, expr
 
 
 def test_query_count_matches_oracle():
