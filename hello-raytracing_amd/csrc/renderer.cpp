@@ -128,8 +128,9 @@ struct rt_renderer {
     DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
-    DevBuf<float4> ring;        // sample-queue fold ring: slots x frames x 64 px (rgb, unused)
-    DevBuf<uint32_t> ring_ctl;  // [0, slots): jobs completed per slot; [slots, 2 slots): folds per slot
+    DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused)
+    DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile done masks (2 words per tile), tile fold lock + cursor
+                                // (2), the free queue (1 per slot) and its tail (4); then the job -> slot map
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
 
@@ -144,6 +145,8 @@ struct rt_renderer {
     uint32_t last_schedule = 0;
     uint32_t last_suspend = 0;
     uint32_t ring_slots = 0;  // fold-ring slots of the last sample-queue draw
+    uint32_t ring_tiles = 0, ring_nchunks = 0;  // (diagnostics: HRT_RING_DUMP)
+    size_t ring_ctl_words = 0;
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
@@ -364,9 +367,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         int rc = upload_spheres(r);  // empty scene: min_sphere_slots zero slots, like an unwritten buffer
         if (rc) return rc;
     }
-    int rc = ensure(r->counter, RT_RAW_COUNTERS);
+    // RT_RAW_COUNTERS exported words, then the sample queue's fold-ring watchdog (rt_kernels.hip idle_spin)
+    int rc = ensure(r->counter, hrt_dev::COUNTER_WORDS);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, RT_RAW_COUNTERS * sizeof(unsigned long long), r->stream));
+    HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, hrt_dev::COUNTER_WORDS * sizeof(unsigned long long), r->stream));
 
     hrt_dev::KParams P{};
     {
@@ -460,28 +464,39 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.tiles_w = (r->width + 7u) / 8u;
         P.tiles_h = (P.nrows + 7u) / 8u;
         const uint32_t ntiles = P.tiles_w * P.tiles_h;
-        // fold ring: a slot (frames x 64 px x 16 B) per tile in flight. Frames per launch: as many as leave room
-        // for RING_MIN_SLOTS slots in the budget; slots: a power of two, at most one per tile. A device short of
-        // memory gets a halved budget (fewer slots, then fewer frames per launch) instead of a failed draw.
-        constexpr uint32_t RING_MIN_SLOTS = 256;
+        // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the heap walk
+        // of the triangle / mixed programs; not the opt-in SAH walk
+        const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
+        // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for k_trace's
+        // cheap sphere scans (C2: 32 costs 3 %); a power of two (the ring's slot layout)
+        uint32_t jf = r->params.job_frames ? r->params.job_frames : (split ? 32u : 16u);
+        P.jf_log2 = 0;
+        while ((2u << P.jf_log2) <= std::min(jf, 1024u)) P.jf_log2++;
+        jf = 1u << P.jf_log2;
+        // frames per launch: at most 64 jobs per tile (the tile's done mask)
+        const uint32_t chunk = std::max(1u, std::min(count, 64u * jf));
+        const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
+        // fold ring: a power-of-two number of job slots (jf x 64 px x 16 B each) in the budget, at most one per
+        // job of a launch. A device short of memory gets a halved budget instead of a failed draw.
         size_t budget = (size_t)std::min<uint32_t>(std::max<uint32_t>(r->params.queue_budget_mb, 1u), 2047u) << 20;
-        uint32_t chunk = 1, log2s = 0;
+        uint32_t log2s = 0;
         auto plan = [&]() {
-            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / ((size_t)RING_MIN_SLOTS << 10)));
-            const size_t fit = std::max<size_t>(1, budget / ((size_t)chunk << 10));
+            const size_t fit = std::max<size_t>(1, budget / ((size_t)jf << 10));
+            const uint64_t jobs = (uint64_t)ntiles * nchunks_max;
             log2s = 0;
-            while ((2ull << log2s) <= fit && (1ull << log2s) < ntiles) log2s++;
-            // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so tiles wait for their slot
+            while ((2ull << log2s) <= fit && (1ull << log2s) < jobs && log2s < 20u) log2s++;
+            // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so jobs wait for their slot
             static const char* cap_env = std::getenv("HRT_RING_SLOTS_MAX");
             if (cap_env)
                 while (log2s > 0 && (1ull << log2s) > std::strtoull(cap_env, nullptr, 10)) log2s--;
         };
         plan();
+        const size_t zero_words = 4ull * ntiles + (4ull << log2s) + 4u;  // (log2s only shrinks below)
         if (count) {
             for (;;) {
-                rc = ensure(r->ring, ((size_t)chunk << log2s) * 64u);
-                if (!rc) rc = ensure(r->ring_ctl, 2ull << log2s);
-                if (rc != RT_ERR_ALLOC || budget <= (64u << 10)) break;
+                rc = ensure(r->ring, ((size_t)jf << log2s) * 64u);
+                if (!rc) rc = ensure(r->ring_ctl, zero_words + (size_t)ntiles * nchunks_max);
+                if (rc != RT_ERR_ALLOC || budget <= ((size_t)jf << 10)) break;
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
                 budget /= 2u;
                 plan();
@@ -490,28 +505,29 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         }
         P.ring = r->ring.ptr;
         P.ring_log2 = log2s;
-        P.ring_bytes = (uint32_t)(((size_t)chunk << log2s) * 1024u);
-        P.ring_done = r->ring_ctl.ptr;
-        P.ring_folds = r->ring_ctl.ptr + (1u << log2s);
+        P.ring_bytes = (uint32_t)(((size_t)jf << log2s) * 1024u);
+        P.tile_done = (unsigned long long*)r->ring_ctl.ptr;
+        P.tile_ctl = r->ring_ctl.ptr + 2ull * ntiles;
+        P.ring_q = r->ring_ctl.ptr + 4ull * ntiles;
+        P.ring_tail = P.ring_q + (4u << log2s);
+        P.job_slot = r->ring_ctl.ptr + zero_words;
         P.queue = r->counter.ptr + 15;
         r->ring_slots = 1u << log2s;
+        r->ring_tiles = ntiles;
+        r->ring_ctl_words = zero_words + (size_t)ntiles * nchunks_max;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
         for (uint32_t done = 0; done < count; done += chunk) {
             P.nframes = std::min(chunk, count - done);
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
-            // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the
-            // heap walk of the triangle / mixed programs; not the opt-in SAH walk
-            const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
-            // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for
-            // k_trace's cheap sphere scans (C2: 32 costs 3 %)
-            P.job_frames = r->params.job_frames ? r->params.job_frames : (split ? 32u : 16u);
+            P.job_frames = jf;
             P.suspend_below = split ? r->params.suspend_below : 0u;
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
             P.njobs = (unsigned long long)ntiles * P.nchunks;
+            r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
-            HIP_TRY(hipMemsetAsync(P.ring_done, 0, (2ull << log2s) * sizeof(uint32_t), r->stream));
+            HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
             rc = trace_events(r, launches);
             if (rc) return rc;
             HIP_TRY(hipEventRecord(r->ev_trace[2 * launches], r->stream));
@@ -540,7 +556,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.local_rows = P.nrows;
     std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
     if (schedule == RT_SCHEDULE_QUEUE && count)
-        r->stats.ring_bytes = (uint64_t)P.ring_bytes + 8ull * r->ring_slots;
+        r->stats.ring_bytes = (uint64_t)P.ring_bytes + 4ull * (4u * r->ring_slots + 4u) +
+                              4ull * P.tiles_w * P.tiles_h * (4u + P.nchunks);
     r->timing_pending = true;
     return RT_OK;
 }
@@ -551,7 +568,32 @@ int finish_stats(rt_renderer* r) {
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
     unsigned long long* q = r->raw_counters;
+    unsigned long long wd[4] = {};
     HIP_TRY(hipMemcpy(q, r->counter.ptr, RT_RAW_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(wd, r->counter.ptr + hrt_dev::WATCHDOG, sizeof wd, hipMemcpyDeviceToHost));
+    if (wd[0] || wd[3]) {  // waves gave up waiting for a fold-ring slot: the image is incomplete; report, do not hang
+        // diagnostics: HRT_RING_DUMP=path writes the fold-ring control words (tile done masks, tile locks and
+        // cursors, free queue, tail) and the counters as raw little-endian words
+        if (const char* path = std::getenv("HRT_RING_DUMP")) {
+            std::vector<uint32_t> ctl(r->ring_ctl_words);
+            if (!ctl.empty())
+                HIP_TRY(hipMemcpy(ctl.data(), r->ring_ctl.ptr, ctl.size() * 4u, hipMemcpyDeviceToHost));
+            unsigned long long cnt[hrt_dev::COUNTER_WORDS];
+            HIP_TRY(hipMemcpy(cnt, r->counter.ptr, sizeof cnt, hipMemcpyDeviceToHost));
+            if (FILE* f = std::fopen(path, "wb")) {
+                const uint32_t hdr[4] = {r->ring_tiles, r->ring_slots, r->ring_nchunks, (uint32_t)ctl.size()};
+                std::fwrite(hdr, 4, 4, f);
+                std::fwrite(cnt, 8, hrt_dev::COUNTER_WORDS, f);
+                std::fwrite(ctl.data(), 4, ctl.size(), f);
+                std::fclose(f);
+            }
+        }
+        char msg[200];
+        std::snprintf(msg, sizeof msg, "sample queue: %llu waves waited > 2^24 idle rounds for a fold-ring slot "
+                      "(last: job %llu, entry flags %llx); %llu free-queue overruns", wd[0], wd[1], wd[2], wd[3]);
+        r->timing_pending = false;
+        return fail(RT_ERR_DEVICE, msg);
+    }
     r->stats.kernel_ms = ms;
     r->stats.trace_ms = ms;
     r->stats.trace_launches = r->stats.launches;

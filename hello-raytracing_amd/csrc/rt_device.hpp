@@ -77,6 +77,10 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 
 // Small culling BVHs (<= LNODE_CAP nodes, depth <= LNODE_DEPTH) are read from LDS by k_trace_split<true>
 // (renderer.cpp decides, the kernel bounds its copy by the same constant).
+// device counter words: [0, 16) exported (include/hrt.h RT_RAW_COUNTERS; [15] = the job queue), then the
+// fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue overruns
+constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
+
 constexpr uint32_t LNODE_CAP = 192;
 constexpr uint32_t LNODE_DEPTH = 8;
 
@@ -132,13 +136,18 @@ struct KParams {
     const MatDev* mats;
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
     unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
-    // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris): the fold ring. A tile's samples go to
-    // ring slot tile % ring_slots; the wave that completes the tile's last job folds them into the image.
-    float4* ring;                 // ring_slots x nframes x 64 px colour (r, g, b, unused)
-    uint32_t* ring_done;          // [slot]: jobs completed in the slot (cumulative over the tiles it holds)
-    uint32_t* ring_folds;         // [slot]: tiles folded out of the slot (the generation allowed to write)
-    uint32_t ring_log2;           // ring_slots = 1 << ring_log2
+    // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris): the fold ring. A job's samples go to a
+    // ring slot taken from a free queue when the job is dealt; each tile's jobs are folded into the image in
+    // order as they complete, and their slots return to the queue.
+    float4* ring;                 // ring_jobs x job_frames x 64 px colour (r, g, b, unused)
+    uint32_t* ring_q;             // [4 ring_jobs]: free queue: slot | (lap & 0x7FF) << 20 | valid << 31
+    uint32_t* ring_tail;          // free-queue tickets issued (slots returned)
+    uint32_t* job_slot;           // [tile * nchunks + chunk]: the job's slot (for its folder)
+    unsigned long long* tile_done;  // [tile]: bit c = the tile's job c has all its samples stored
+    uint32_t* tile_ctl;           // [tile]: fold lock, jobs folded (2 words)
+    uint32_t ring_log2;           // ring_jobs = 1 << ring_log2 (<= 2^20)
     uint32_t ring_bytes;          // size of `ring` (buffer-descriptor range)
+    uint32_t jf_log2, pad_r;      // job_frames = 1 << jf_log2
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows

@@ -878,102 +878,139 @@ __device__ __forceinline__ LaneLists lane_lists() {
 
 // ---- The fold ring (sample queue) ----
 // A job is one 8x8 tile x job_frames frames, taken by ONE wave from the queue; a tile's jobs are dealt one
-// after another (tile-major), so they run at once on neighbouring waves. Each sample's colour goes to the
-// tile's ring slot (slot = tile % ring_slots, frame-major, 16 B per pixel) as a write-through (sc1) store.
-// A wave tracks its jobs (WaveJobs); when every sample of one has been stored it drains its stores
-// (s_waitcnt vmcnt(0)) and adds 1 to the slot's job count (agent-scope atomic). The wave whose add completes
-// the tile folds the slot into the image, frame by frame in order (the expression of k_render; sc1 loads
-// behind an agent acquire), then releases the slot to the tile ring_slots further on, whose jobs wait for
-// it. Memory is O(tiles in flight) instead of O(frames x pixels), and there is no separate fold pass.
-// Hand-off form: MI355X_MICROARCH.md § visibility, row 1 of the sc1 table (the storing unit is the wave:
-// all a job's samples are stored by the wave that dealt it).
+// after another (tile-major), so they run at once on neighbouring waves. A job takes a ring slot from a free
+// queue when it is dealt (job j takes the (j - ring_jobs)-th returned slot, so slots go out in job order and a
+// job never waits on a later one), and each sample's colour goes to its job's slot (frame-major, 16 B per
+// pixel) as a write-through (sc1) store. A wave tracks
+// its jobs (WaveJobs); when every sample of one has been stored it drains its stores (s_waitcnt vmcnt(0)), sets
+// the job's bit in the tile's done mask and tries the tile's fold lock. The lock holder folds the tile's jobs
+// in order, as far as they are done, into the image (the expression of k_render, frame by frame; sc1 loads and
+// stores), returns their slots, releases the lock and re-checks the mask (a job that completed meanwhile found
+// the lock taken and left its fold to the holder). So folding trails each tile's slowest job by one job's fold,
+// memory is O(jobs in flight) instead of O(frames x pixels), and there is no separate fold pass.
+// Hand-off form: MI355X_MICROARCH.md § visibility, row 1 of the sc1 table (the storing unit is the wave, which
+// drains before its atomic; the consumer learns by the value an atomic returned; every load of handed-off
+// bytes, slot or image, is an sc1 load).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc() {
     const KPtr K = kargs();
     return __builtin_amdgcn_make_buffer_rsrc((void*)K->ring, (short)0, (int)K->ring_bytes, 0x00020000);
 }
 
-__device__ __forceinline__ void ring_store(uint32_t pix, uint32_t fl, const f3 c) {
-    const KPtr K = kargs();
-    const uint32_t slot = (pix >> 6) & ((1u << K->ring_log2) - 1u);
-    const uint32_t off = (((slot * K->nframes + fl) << 6) | (pix & 63u)) << 4;
-    const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
-    __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16 /* sc1: write-through */);
+// Free-queue entry of return m (m-th slot returned; taken by job ticket m + ring_jobs): the slot, the lap of the
+// queue (4 x ring_jobs entries) it was written in, valid bit. A waiting job polls its entry every round, so the
+// entry is taken long before return m + 4 ring_jobs overwrites it (an overwrite is detected, never misread).
+__device__ __forceinline__ uint32_t ring_q_entry(uint32_t slot, uint32_t m, uint32_t ring_log2) {
+    return slot | ((((m >> (ring_log2 + 2u)) + 1u) & 0x7FFu) << 20) | 0x80000000u;
 }
 
-// Folds tile `tile`'s slot (all P.nframes frames, in order) into the image; the whole wave, lane = pixel.
-__device__ __forceinline__ void fold_tile(uint32_t tile) {
+// Byte offset of (slot, frame within the job, pixel) in the ring.
+__device__ __forceinline__ uint32_t ring_off(uint32_t slot, uint32_t fj, uint32_t px, uint32_t jf_log2) {
+    return (((slot << jf_log2) + fj) << 10) | (px << 4);
+}
+
+// Folds job `c` of tile `tile` (its frames, in order) into the image; the whole wave, lane = pixel. Then frees
+// the job's slot.
+__device__ __forceinline__ void fold_job(uint32_t tile, uint32_t c, uint32_t lane) {
     const KPtr K = kargs();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t slot = tile & ((1u << K->ring_log2) - 1u);
     const uint32_t x = (tile % K->tiles_w) * 8u + (lane & 7u);
     const uint32_t kr = (tile / K->tiles_w) * 8u + (lane >> 3);
     const bool ok = x < K->W && kr < K->nrows;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     float* px = K->image + ((size_t)(ok ? kr : 0u) * K->W + (ok ? x : 0u)) * 3u;
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
     if (ok) {
-        a0 = px[0];
-        a1 = px[1];
-        a2 = px[2];
+        a0 = __hip_atomic_load(px + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a1 = __hip_atomic_load(px + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a2 = __hip_atomic_load(px + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const __amdgpu_buffer_rsrc_t rs = ring_rsrc();
-    const uint32_t nf = K->nframes, frame0 = K->frame0;
+    uint32_t slot = 0;
+    if (lane == 0) slot = __hip_atomic_load(K->job_slot + tile * K->nchunks + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slot = uniform(__shfl(slot, 0));
+    const uint32_t f0 = c << K->jf_log2, nf = min(1u << K->jf_log2, K->nframes - f0);
+    const uint32_t frame0 = K->frame0 + f0;
     const float cap = K->ema_cap;
-    uint32_t off = ((slot * nf) << 10) | (lane << 4);
-    constexpr uint32_t U = 2;
+    uint32_t off = ring_off(slot, 0u, lane, K->jf_log2);
+    constexpr uint32_t U = 1;
     uint32_t f = 0;
+#ifdef HRT_EXP_NOFOLD
+    f = nf;
+#endif
     for (; f + U <= nf; f += U) {
-        u32x4 c[U];
+        u32x4 v[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) c[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + (u << 10)), 0, 16);
+        for (uint32_t u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + (u << 10)), 0, 16);
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             const float w = 1.0f / (fmin_ieee((float)(frame0 + f + u), cap) + 1.0f);
             const float omw = 1.0f - w;
-            a0 = a0 * omw + (0.0f + __uint_as_float(c[u].x)) * w;
-            a1 = a1 * omw + (0.0f + __uint_as_float(c[u].y)) * w;
-            a2 = a2 * omw + (0.0f + __uint_as_float(c[u].z)) * w;
+            a0 = a0 * omw + (0.0f + __uint_as_float(v[u].x)) * w;
+            a1 = a1 * omw + (0.0f + __uint_as_float(v[u].y)) * w;
+            a2 = a2 * omw + (0.0f + __uint_as_float(v[u].z)) * w;
         }
         off += U << 10;
     }
     for (; f < nf; f++, off += 1u << 10) {
-        const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
         const float w = 1.0f / (fmin_ieee((float)(frame0 + f), cap) + 1.0f);
         const float omw = 1.0f - w;
-        a0 = a0 * omw + (0.0f + __uint_as_float(c.x)) * w;
-        a1 = a1 * omw + (0.0f + __uint_as_float(c.y)) * w;
-        a2 = a2 * omw + (0.0f + __uint_as_float(c.z)) * w;
+        a0 = a0 * omw + (0.0f + __uint_as_float(v.x)) * w;
+        a1 = a1 * omw + (0.0f + __uint_as_float(v.y)) * w;
+        a2 = a2 * omw + (0.0f + __uint_as_float(v.z)) * w;
     }
     if (ok) {
-        px[0] = a0;
-        px[1] = a1;
-        px[2] = a2;
+        __hip_atomic_store(px + 0, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(px + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(px + 2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // every load of the slot has returned (its values are folded); then the slot passes to the next tile
+    // every load of the slot has returned (its values are folded): return the slot to the free queue, for the
+    // job whose ticket is this return's + ring_jobs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(K->ring_folds + slot, (tile >> K->ring_log2) + 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        const uint32_t m = __hip_atomic_fetch_add(K->ring_tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(K->ring_q + (m & ((4u << K->ring_log2) - 1u)), ring_q_entry(slot, m, K->ring_log2),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
-
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // The wave's jobs whose samples are not all stored yet: the current one (being dealt, or waiting for its ring
 // slot) and up to WJ_NE - 1 older ones with samples still in flight (a 50-bounce path can outlive several
 // jobs of its wave). Kept in LDS, one block of words per wave (every lane reads and writes the same values),
 // not in registers: the walk kernels have no SGPRs to spare.
 constexpr uint32_t WJ_NE = 4;
-enum : uint32_t { WJ_TILE = 0, WJ_F0 = WJ_NE, WJ_LIVE = 2 * WJ_NE, WJ_FLAGS = 3 * WJ_NE, WJ_STAT = 3 * WJ_NE + 1 };
+// per entry: tile, first frame, samples in flight, ring slot (the job id while waiting for one)
+enum : uint32_t { WJ_TILE = 0, WJ_F0 = WJ_NE, WJ_LIVE = 2 * WJ_NE, WJ_SLOT = 3 * WJ_NE, WJ_FLAGS = 4 * WJ_NE,
+                  WJ_IDLE = 4 * WJ_NE + 1, WJ_STAT = 4 * WJ_NE + 2 };
 // flags: busy bit per entry (bits 0..WJ_NE-1), the current entry (bits 8-9), dealing, waiting
-enum : uint32_t { WJ_BUSY = (1u << WJ_NE) - 1u, WJ_CUR_SHIFT = 8, WJ_DEALING = 1u << 12, WJ_WAITING = 1u << 13 };
+// (slotted: the waiting current job has its slot)
+enum : uint32_t { WJ_BUSY = (1u << WJ_NE) - 1u, WJ_CUR_SHIFT = 8, WJ_DEALING = 1u << 12, WJ_WAITING = 1u << 13,
+                  WJ_SLOTTED = 1u << 14 };
 struct WaveJobs {
     uint32_t* w;  // this wave's words
     __device__ uint32_t get(uint32_t i) const { return uniform(w[i]); }
     __device__ void set(uint32_t i, uint32_t v) const { w[i] = v; }
     __device__ bool dealing() const { return (get(WJ_FLAGS) & WJ_DEALING) != 0u; }
     __device__ bool idle() const { return (get(WJ_FLAGS) & WJ_BUSY) == 0u; }
+    __device__ uint32_t cur() const { return (get(WJ_FLAGS) >> WJ_CUR_SHIFT) & 3u; }
 };
+
+// A dealt sample's job reference (`fl` in the kernels): its wave's entry and its frame within the job.
+__device__ __forceinline__ uint32_t sample_ref(uint32_t entry, uint32_t fj) { return (entry << 16) | fj; }
+
+__device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint32_t ref, const f3 c) {
+    const KPtr K = kargs();
+    const uint32_t slot = J.w[WJ_SLOT + (ref >> 16)];  // per-lane entry: an LDS read, not a uniform value
+    const uint32_t off = ring_off(slot, ref & 0xFFFFu, pix & 63u, K->jf_log2);
+    const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
+#ifndef HRT_EXP_NOSTORE
+    __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16 /* sc1: write-through */);
+#else
+    if (__float_as_uint(c.x) == 0x7FC00001u) __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16);
+#endif
+}
 
 #ifdef HRT_RINGSTAT
 // diagnostic build: per-wave ring statistics (stall rounds: every entry busy; slot-wait rounds; folds; fold
@@ -994,21 +1031,93 @@ __device__ __forceinline__ WaveJobs wave_jobs(uint32_t* lds) {
     return J;
 }
 
-// One job of the wave is complete (every sample stored): count it in its slot. true: it completed the tile, which
-// the wave must now fold.
-__device__ __forceinline__ bool job_complete(uint32_t tile, uint32_t lane) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores have reached memory
+// A round with nothing in flight (the current job waits for a ring slot): sleep. A wave idle for 2^24 rounds in
+// a row (seconds) would mean a broken protocol: it records itself in the watchdog words and leaves (true), so
+// the launch ends and the draw reports an error instead of hanging the device. Any round with work resets it.
+__device__ __forceinline__ bool idle_spin(const WaveJobs& J, uint32_t lane) {
+    __builtin_amdgcn_s_sleep(2);
+    const uint32_t n = J.get(WJ_IDLE) + 1u;
+    J.set(WJ_IDLE, n);
+    if (n < (1u << 24)) return false;
+    if (lane == 0) {
+        const KPtr K = kargs();
+        atomicAdd(K->counter + WATCHDOG, 1ull);
+        atomicExch(K->counter + WATCHDOG + 1, (unsigned long long)J.get(WJ_SLOT + J.cur()));
+        atomicExch(K->counter + WATCHDOG + 2, (unsigned long long)J.get(WJ_FLAGS));
+    }
+    return true;
+}
+
+// One job of the wave is complete (every sample stored): mark it in the tile's done mask, then fold the tile as
+// far as its jobs are done if the fold lock is free (else its holder folds this job).
+__device__ __forceinline__ void job_complete(uint32_t tile, uint32_t c, uint32_t slot, uint32_t lane) {
     const KPtr K = kargs();
-    const uint32_t slot = tile & ((1u << K->ring_log2) - 1u);
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(K->ring_done + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = uniform(__shfl(old, 0));
-    return old + 1u == ((tile >> K->ring_log2) + 1u) * K->nchunks;
+    if (lane == 0) __hip_atomic_store(K->job_slot + tile * K->nchunks + c, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores (and the slot) have reached memory
+    if (lane == 0) __hip_atomic_fetch_or(K->tile_done + tile, 1ull << c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the bit must be set before the lock is tried: a holder that releases after our failed try re-reads the mask
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t* lock = K->tile_ctl + 2u * tile;
+#pragma nounroll
+    while (true) {
+        uint32_t held = 0;
+        if (lane == 0) held = __hip_atomic_fetch_or(lock, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (uniform(__shfl(held, 0)) != 0u) return;  // the holder re-checks the mask after releasing
+        uint32_t p = 0;
+        unsigned long long m = 0;
+        if (lane == 0) {
+            p = __hip_atomic_load(lock + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m = __hip_atomic_load(K->tile_done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        p = uniform(__shfl(p, 0));
+        m = ((unsigned long long)uniform(__shfl((uint32_t)(m >> 32), 0)) << 32) | uniform(__shfl((uint32_t)m, 0));
+        const uint32_t nc = K->nchunks;
+#pragma nounroll
+        while (p < nc && ((m >> p) & 1ull)) {
+            fold_job(tile, p, lane);
+            p++;
+        }
+        if (lane == 0) __hip_atomic_store(lock + 1, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image, slot and cursor stores before the release
+        if (lane == 0) __hip_atomic_store(lock, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p >= nc) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the release before the re-check
+        if (lane == 0) m = __hip_atomic_load(K->tile_done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t bit = (uint32_t)(m >> p) & 1u;
+        if (uniform(__shfl(bit, 0)) == 0u) return;  // job p not done yet: its wave folds it
+    }
 }
 
 // The current job is dealt out (it completes in job_account once nothing of it is in flight).
 __device__ __forceinline__ void job_close(const WaveJobs& J, uint32_t /*lane*/) {
     J.set(WJ_FLAGS, J.get(WJ_FLAGS) & ~WJ_DEALING);
+}
+
+// The waiting current job polls the free queue for its slot (job j >= ring_jobs takes return j - ring_jobs).
+__device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uint32_t lane) {
+    if (flags & WJ_SLOTTED) return true;
+    const KPtr K = kargs();
+    const uint32_t cur = (flags >> WJ_CUR_SHIFT) & 3u;
+    const uint32_t job = J.get(WJ_SLOT + cur);  // waiting: the job id is its free-queue ticket
+    uint32_t slot = job;                        // the first ring_jobs jobs take the slots in order
+    if (job >> K->ring_log2) {
+        const uint32_t m = job - (1u << K->ring_log2);
+        uint32_t v = 0;
+        if (lane == 0) v = __hip_atomic_load(K->ring_q + (m & ((4u << K->ring_log2) - 1u)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        v = uniform(__shfl(v, 0));
+        const uint32_t want = ring_q_entry(0u, m, K->ring_log2);
+        if ((v & 0xFFF00000u) != want) {  // not returned yet (or, never expected, already overwritten)
+            if ((v & 0x80000000u) && (((v >> 20) - (want >> 20)) & 0x7FFu) < 0x400u && lane == 0)
+                atomicAdd(K->counter + WATCHDOG + 3, 1ull);
+            RINGSTAT_ADD(J, 1, 1);
+            return false;
+        }
+        slot = v & 0xFFFFFu;
+    }
+    J.set(WJ_SLOT + cur, slot);
+    J.set(WJ_FLAGS, flags | WJ_SLOTTED);
+    return true;
 }
 
 // Makes a job current and dealable: fetch one into a free entry and wait for its slot.
@@ -1033,22 +1142,14 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
         J.set(WJ_TILE + e, j / K->nchunks);
         J.set(WJ_F0 + e, (j % K->nchunks) * K->job_frames);
         J.set(WJ_LIVE + e, 0u);
-        flags = (flags & ~(3u << WJ_CUR_SHIFT)) | (1u << e) | (e << WJ_CUR_SHIFT) | WJ_WAITING;
+        J.set(WJ_SLOT + e, j);
+        flags = (flags & ~((3u << WJ_CUR_SHIFT) | WJ_SLOTTED)) | (1u << e) | (e << WJ_CUR_SHIFT) | WJ_WAITING;
         J.set(WJ_FLAGS, flags);
     }
+    if (!slot_poll(J, flags, lane)) return false;
     const uint32_t cur = (flags >> WJ_CUR_SHIFT) & 3u;
-    const uint32_t t = J.get(WJ_TILE + cur);
-    uint32_t folds = 0;
-    if (lane == 0)
-        folds = __hip_atomic_load(K->ring_folds + (t & ((1u << K->ring_log2) - 1u)), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-    folds = uniform(__shfl(folds, 0));
-    if (folds < (t >> K->ring_log2)) {  // the slot's previous tile is not folded yet
-        RINGSTAT_ADD(J, 1, 1);
-        return false;
-    }
-    J.set(WJ_FLAGS, (flags & ~WJ_WAITING) | WJ_DEALING);
-    job_tile = t;
+    J.set(WJ_FLAGS, (flags & ~(WJ_WAITING | WJ_SLOTTED)) | WJ_DEALING);
+    job_tile = J.get(WJ_TILE + cur);
     job_f0 = J.get(WJ_F0 + cur);
     job_nf = min(K->job_frames, K->nframes - job_f0);
     return true;
@@ -1057,6 +1158,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
 // Samples just dealt from the current job (lanes that took one).
 __device__ __forceinline__ void job_dealt(const WaveJobs& J, uint32_t n) {
     if (n == 0u) return;
+    J.set(WJ_IDLE, 0u);
     const uint32_t i = WJ_LIVE + ((J.get(WJ_FLAGS) >> WJ_CUR_SHIFT) & 3u);
     J.set(i, J.get(i) + n);
 }
@@ -1064,21 +1166,19 @@ __device__ __forceinline__ void job_dealt(const WaveJobs& J, uint32_t n) {
 // End of a round: lanes whose sample finished (`fin`, colour stored) are counted off their jobs (the busy entry
 // whose tile and frames hold the sample); jobs neither current nor with anything in flight complete, and a job
 // that completes its tile folds it.
-__device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_t pix, uint32_t fl, uint32_t lane) {
+__device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_t ref, uint32_t lane) {
     const unsigned long long any = __ballot(fin);
     if (any != 0ull) {
-        const KPtr K = kargs();
-        const uint32_t busy = J.get(WJ_FLAGS) & WJ_BUSY;
-        uint32_t idx = 0;
-#pragma unroll
-        for (uint32_t e = 1; e < WJ_NE; e++)
-            if (((busy >> e) & 1u) && (pix >> 6) == J.get(WJ_TILE + e) && fl - J.get(WJ_F0 + e) < K->job_frames)
-                idx = e;
+        const uint32_t idx = ref >> 16;
 #pragma unroll
         for (uint32_t e = 0; e < WJ_NE; e++) {
             const uint32_t n = (uint32_t)__popcll(__ballot(fin && idx == e));
             if (n) J.set(WJ_LIVE + e, J.get(WJ_LIVE + e) - n);
         }
+    }
+    {
+        const uint32_t flags = J.get(WJ_FLAGS);
+        if (flags & WJ_WAITING) (void)slot_poll(J, flags, lane);  // every round, not only when lanes are free
     }
 #pragma nounroll
     for (uint32_t e = 0; e < WJ_NE; e++) {
@@ -1086,17 +1186,14 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
         const bool current = ((flags >> WJ_CUR_SHIFT) & 3u) == e && (flags & (WJ_DEALING | WJ_WAITING));
         if (((flags >> e) & 1u) && J.get(WJ_LIVE + e) == 0u && !current) {
             J.set(WJ_FLAGS, flags & ~(1u << e));
-            const uint32_t t = J.get(WJ_TILE + e);
-            if (job_complete(t, lane)) {
 #ifdef HRT_RINGSTAT
-                const unsigned long long t0 = __builtin_readcyclecounter();
+            const unsigned long long t0 = __builtin_readcyclecounter();
 #endif
-                fold_tile(t);
+            job_complete(J.get(WJ_TILE + e), J.get(WJ_F0 + e) >> kargs()->jf_log2, J.get(WJ_SLOT + e), lane);
 #ifdef HRT_RINGSTAT
-                RINGSTAT_ADD(J, 2, 1);
-                RINGSTAT_ADD(J, 3, (__builtin_readcyclecounter() - t0) >> 4);
+            RINGSTAT_ADD(J, 2, 1);
+            RINGSTAT_ADD(J, 3, (__builtin_readcyclecounter() - t0) >> 4);
 #endif
-            }
         }
     }
 }
@@ -1152,7 +1249,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
                 ray.o = mk(ox, oy, oz);
                 ray.d = mk(dx, dy, dz);
                 s = ss;
-                fl = B.job_f0 + B.blk_f;
+                fl = sample_ref(J.cur(), B.blk_f);
                 pix = B.job_tile * 64u + (uint32_t)src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
                 att = mk(1.0f, 1.0f, 1.0f);
@@ -1328,7 +1425,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // coherence: an incoherent sample queue measured 2.65x slower on C3), and one tile's frames are
 // spread over many waves. Each sample's colour goes to its tile's slot of the fold ring, and the wave that
 // completes a tile's last job folds the slot into the image in frame order per pixel with the reference's
-// mix (shader_sphere.wgsl:264-271; fold_tile), so the image is bit-identical to k_render's and to
+// mix (shader_sphere.wgsl:264-271; fold_job), so the image is bit-identical to k_render's and to
 // count x rt_draw.
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
@@ -1390,14 +1487,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             if (need && rank < avail) {
                 const uint32_t sid = job_next + rank;
                 const uint32_t l = sid & 63u;
-                fl = job_f0 + (sid >> 6);
+                fl = sample_ref(J.cur(), sid >> 6);
                 pix = job_tile * 64u + l;
                 const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
                 const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
                 need = false;
                 if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
                     const uint32_t y = P.row0 + kr * P.row_step;
-                    ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + fl * P.dtime, s);
+                    ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (job_f0 + (sid >> 6)) * P.dtime, s);
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
                     bounce = 0;
@@ -1417,7 +1514,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #endif
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
-            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+            if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
         }
         bool fin = false;
         bool done = have;
@@ -1450,14 +1547,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             const float u = 1.0f - sky_t;
             const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
             const f3 c = att * sky;
-            ring_store(pix, fl, c);
+            ring_store(J, pix, fl, c);
             have = false;
             fin = true;
         }
 #ifdef HRT_STAMPS
         st_shade += hrt_stamp() - st_tb;
 #endif
-        job_account(J, fin, pix, fl, lane);
+        job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
     {
@@ -1551,7 +1648,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 ray.o = mk(b0.x, b0.y, b0.z);
                 ray.d = mk(b0.w, b1.x, b1.y);
                 s = __float_as_uint(b1.z);
-                fl = B.job_f0 + B.blk_f;
+                fl = sample_ref(J.cur(), B.blk_f);
                 pix = B.job_tile * 64u + src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
                 att = mk(1.0f, 1.0f, 1.0f);
@@ -1657,7 +1754,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     ray.o = mk(ox, oy, oz);
                     ray.d = mk(dx, dy, dz);
                     s = ss;
-                    fl = job_f0 + blk_f;
+                    fl = sample_ref(J.cur(), blk_f);
                     pix = job_tile * 64u + (uint32_t)src;
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
@@ -1674,7 +1771,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         }
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
-            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+            if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
         }
         bool fin = false;
 #ifdef HRT_STAMPS
@@ -1718,13 +1815,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                ring_store(pix, fl, c);
+                ring_store(J, pix, fl, c);
                 have = false;
                 fin = true;
             }
             qs = 0u;
         }
-        job_account(J, fin, pix, fl, lane);
+        job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
     {
@@ -1799,7 +1896,7 @@ k_trace_split_tris(const KParams P) {
         refill_block_lds<MODE>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
-            if (!drained) __builtin_amdgcn_s_sleep(2);  // nothing in flight: the next job waits for its ring slot
+            if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
         }
         bool fin = false;
         if (have && qs == 0u) {
@@ -1842,13 +1939,13 @@ k_trace_split_tris(const KParams P) {
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                ring_store(pix, fl, c);
+                ring_store(J, pix, fl, c);
                 have = false;
                 fin = true;
             }
             qs = 0u;
         }
-        job_account(J, fin, pix, fl, lane);
+        job_account(J, fin, fl, lane);
     }
 #ifdef HRT_RINGSTAT
     if (lane == 0)
