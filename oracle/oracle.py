@@ -24,19 +24,20 @@ class OParams(C.Structure):
                                           "step_cap")]
 
 
-_lib = None
+_libs: dict = {}
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", os.fspath(HERE)], check=True)
 
 
-def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
-            build()
-        L = C.CDLL(os.fspath(LIB))
+def lib(contract: int = 0) -> C.CDLL:
+    """The oracle library; contract 1-5 = the float-contract study variants (rt_oracle.c ORACLE_CONTRACT)."""
+    if contract not in _libs:
+        path = LIB if contract == 0 else HERE / "build" / f"liboracle_c{contract}.so"
+        if not path.exists():
+            subprocess.run(["make", "-s", "-C", os.fspath(HERE), "all" if contract == 0 else "contracts"], check=True)
+        L = C.CDLL(os.fspath(path))
         L.oracle_render.restype = C.c_uint64
         L.oracle_render.argtypes = [C.POINTER(OParams), C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -44,15 +45,15 @@ def lib() -> C.CDLL:
         L.oracle_sizeof.restype = C.c_uint32
         L.oracle_sizeof.argtypes = [C.c_int]
         assert [L.oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
-        _lib = L
-    return _lib
+        _libs[contract] = L
+    return _libs[contract]
 
 
 def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: int, time0: int = 1000,
            dtime: int = 10, frame0: int = 0, bounces: int | None = None, ema_cap: int = 1000,
            spheres: np.ndarray | None = None, min_sphere_slots: int | None = None, bvh=None,
            rows=None, x0: int = 0, nx: int | None = None, image: np.ndarray | None = None,
-           threads: int = 0, step_cap: int = 600):
+           threads: int = 0, step_cap: int = 600, contract: int = 0):
     """Render `frames` frames (time0 + f*dtime, frame_count frame0 + f) of a scene.
 
     spheres: SPHERE_DTYPE array (zero slots appended up to min_sphere_slots, default 100 in sphere mode
@@ -100,7 +101,7 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
     if threads <= 0:  # explicit: importing torch can leave the OpenMP default at one thread
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     counts = (C.c_uint64 * 4)()
-    q = lib().oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
+    q = lib(contract).oracle_render(C.byref(p), cam, sph_ptr, nslots, sizes_p, nodes_p, tris_p, mats_p,
                             image.ctypes.data, threads, counts)
     last_counts.update(rays=counts[0], node_tests=counts[1], tri_tests=counts[2], capped_walks=counts[3])
     return image, int(q)

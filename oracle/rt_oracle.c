@@ -37,6 +37,30 @@
 
 #define FLT_MAX_REF 3.40282e+38f /* shader_*.wgsl:4 */
 
+/*
+ * Float-contract study (tests/golden/contract_study.py): the reference GPU's compiler may fuse
+ * or reassociate differently. ORACLE_CONTRACT selects a variant at build time; 0 (the default, and the only
+ * one the kernels implement) is the contract above.
+ *   1: no fused multiply-add anywhere (dot products, discriminant, point_on_ray unfused);
+ *   2: contract 0 plus every a*b+c of the shaders fused (make_ray, mix, reflect, refract, reflectance, sky, c);
+ *   3: contract 0 with normalize(v) = v * (1 / sqrt(dot(v, v)));
+ *   4: contracts 2 and 3 together;
+ *   5: every division by a computed value as a * (1 / b) (the reciprocal-based division GPU compilers emit
+ *      for WGSL's 2.5-ulp `/`), normalize included.
+ */
+#ifndef ORACLE_CONTRACT
+#define ORACLE_CONTRACT 0
+#endif
+#define OC_NOFMA (ORACLE_CONTRACT == 1)
+#define OC_FUSE (ORACLE_CONTRACT == 2 || ORACLE_CONTRACT == 4)
+#define OC_RCPNORM (ORACLE_CONTRACT == 3 || ORACLE_CONTRACT == 4 || ORACLE_CONTRACT == 5)
+#define OC_RCPDIV (ORACLE_CONTRACT == 5)
+static inline float fmaf_c(float a, float b, float c) { return OC_NOFMA ? a * b + c : fmaf(a, b, c); }
+/* a*b + c at the sites a compiler may fuse */
+static inline float madd(float a, float b, float c) { return OC_FUSE ? fmaf(a, b, c) : a * b + c; }
+/* a / b at the sites whose divisor is computed */
+static inline float divf(float a, float b) { return OC_RCPDIV ? a * (1.0f / b) : a / b; }
+
 enum { MODE_SPHERE = 0, MODE_TRIS = 1, MODE_MIXED = 2 };
 
 /* ---- reference POD layouts (bytemuck #[repr(C)]), src/scene/{camera,material,sphere}.rs, bvh/ ---- */
@@ -67,9 +91,13 @@ static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
 static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
 static inline v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
-static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline float dot3(v3 a, v3 b) { return fmaf_c(a.z, b.z, fmaf_c(a.y, b.y, a.x * b.x)); }
 static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
-static inline v3 norm3(v3 a) { float l = len3(a); return V(a.x / l, a.y / l, a.z / l); }
+static inline v3 norm3(v3 a) {
+    float l = len3(a);
+    if (OC_RCPNORM) { float r = 1.0f / l; return V(a.x * r, a.y * r, a.z * r); }
+    return V(a.x / l, a.y / l, a.z / l);
+}
 static inline v3 cross3(v3 a, v3 b) {
     return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -112,19 +140,18 @@ static ray_t make_ray(const o_scene *sc, float ux, float uy, uint32_t *s) {
     float v[4], d4[4], f4[4], o4[4];
     for (int i = 0; i < 4; i++) {
         float xx = (c->right[i] * ux) * sc->k;
-        float yy = (c->up[i] * uy) * sc->k;
-        v[i] = (xx + yy) + c->dir[i];
+        v[i] = madd(c->up[i] * uy, sc->k, xx) + c->dir[i];
     }
-    float l = sqrtf(fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0]))));
-    for (int i = 0; i < 4; i++) d4[i] = v[i] / l;
-    for (int i = 0; i < 4; i++) f4[i] = c->eye[i] + d4[i] * c->params[0];
+    float l = sqrtf(fmaf_c(v[3], v[3], fmaf_c(v[2], v[2], fmaf_c(v[1], v[1], v[0] * v[0]))));
+    for (int i = 0; i < 4; i++) d4[i] = OC_RCPNORM ? v[i] * (1.0f / l) : v[i] / l;
+    for (int i = 0; i < 4; i++) f4[i] = madd(d4[i], c->params[0], c->eye[i]);
     /* random_on_disk: shader_sphere.wgsl:118-122 */
     float r1 = rng_float(s), r2 = rng_float(s);
-    float l2 = sqrtf(fmaf(r2, r2, r1 * r1));
-    float vx = r1 / l2, vy = r2 / l2;
+    float l2 = sqrtf(fmaf_c(r2, r2, r1 * r1));
+    float vx = OC_RCPNORM ? r1 * (1.0f / l2) : r1 / l2, vy = OC_RCPNORM ? r2 * (1.0f / l2) : r2 / l2;
     float rr = rng_float(s) * c->params[1];
-    o4[0] = c->eye[0] + vx * rr;
-    o4[1] = c->eye[1] + vy * rr;
+    o4[0] = madd(vx, rr, c->eye[0]);
+    o4[1] = madd(vy, rr, c->eye[1]);
     o4[2] = c->eye[2] + 0.0f * rr;
     o4[3] = c->eye[3] + 1.0f;
     ray_t r;
@@ -134,8 +161,9 @@ static ray_t make_ray(const o_scene *sc, float ux, float uy, uint32_t *s) {
     } else {
         float g[4];
         for (int i = 0; i < 4; i++) g[i] = f4[i] - o4[i];
-        float lg = sqrtf(fmaf(g[3], g[3], fmaf(g[2], g[2], fmaf(g[1], g[1], g[0] * g[0]))));
-        r.d = V(g[0] / lg, g[1] / lg, g[2] / lg);
+        float lg = sqrtf(fmaf_c(g[3], g[3], fmaf_c(g[2], g[2], fmaf_c(g[1], g[1], g[0] * g[0]))));
+        r.d = OC_RCPNORM ? V(g[0] * (1.0f / lg), g[1] * (1.0f / lg), g[2] * (1.0f / lg))
+                         : V(g[0] / lg, g[1] / lg, g[2] / lg);
     }
     return r;
 }
@@ -150,17 +178,17 @@ static void closest_sphere(const o_scene *sc, ray_t r, hit_t *h) {
         const o_sphere *sp = &sc->spheres[i];
         v3 oc = vsub(r.o, ld3(sp->center));
         float b = 2.0f * dot3(oc, r.d);
-        float c = dot3(oc, oc) - sp->radius * sp->radius;
-        float disc = fmaf(b, b, -((4.0f * a) * c));
+        float c = OC_FUSE ? fmaf(-sp->radius, sp->radius, dot3(oc, oc)) : dot3(oc, oc) - sp->radius * sp->radius;
+        float disc = fmaf_c(b, b, -((4.0f * a) * c));
         if (disc < 0.0f) continue; /* t = -1 */
-        float t = (-b - sqrtf(disc)) / (2.0f * a);
+        float t = divf(-b - sqrtf(disc), 2.0f * a);
         if (t > 0.0f && t < best) { best = t; idx = (int)i; }
     }
     if (idx < 0) return;
     const o_sphere *sp = &sc->spheres[idx];
-    v3 p = V(fmaf(best, r.d.x, r.o.x), fmaf(best, r.d.y, r.o.y), fmaf(best, r.d.z, r.o.z));
+    v3 p = V(fmaf_c(best, r.d.x, r.o.x), fmaf_c(best, r.d.y, r.o.y), fmaf_c(best, r.d.z, r.o.z));
     v3 n = vsub(p, ld3(sp->center));
-    n = V(n.x / sp->radius, n.y / sp->radius, n.z / sp->radius);
+    n = V(divf(n.x, sp->radius), divf(n.y, sp->radius), divf(n.z, sp->radius));
     int front = dot3(r.d, n) < 0.0f;
     if (!front) n = vneg(n);
     h->p = p; h->n = n; h->t = best; h->mat = &sp->mat; h->front = front;
@@ -192,7 +220,7 @@ static inline void tri_test(const o_scene *sc, ray_t r, uint32_t j, hit_t *h) {
     if (v < 0.0f || u + v > 1.0f) return;
     float t = inv_det * dot3(e2, q);
     if (t < 1e-4f || t >= h->t) return;
-    h->p = V(fmaf(t, r.d.x, r.o.x), fmaf(t, r.d.y, r.o.y), fmaf(t, r.d.z, r.o.z));
+    h->p = V(fmaf_c(t, r.d.x, r.o.x), fmaf_c(t, r.d.y, r.o.y), fmaf_c(t, r.d.z, r.o.z));
     h->n = ld3(tr->normal);
     h->t = t;
     h->mat = &sc->mats[tr->material];
@@ -224,20 +252,24 @@ static void closest_bvh(const o_scene *sc, ray_t r, hit_t *h, uint64_t *cnt) {
     if (step == cap && i != 0u) cnt[3]++; /* walks the step cap cut short (bookkeeping, not semantics) */
 }
 
-static inline v3 reflect3(v3 v, v3 n) { return vsub(v, smul(2.0f * dot3(v, n), n)); }
+static inline v3 reflect3(v3 v, v3 n) {
+    float k = 2.0f * dot3(v, n);
+    if (OC_FUSE) return V(fmaf(-k, n.x, v.x), fmaf(-k, n.y, v.y), fmaf(-k, n.z, v.z));
+    return vsub(v, smul(k, n));
+}
 static inline v3 refract3(v3 uv, v3 n, float e) { /* shader_sphere.wgsl:159-165 */
     float cos_t = fminf(dot3(vneg(uv), n), 1.0f);
-    v3 perp = smul(e, vadd(uv, smul(cos_t, n)));
+    v3 perp = smul(e, V(madd(cos_t, n.x, uv.x), madd(cos_t, n.y, uv.y), madd(cos_t, n.z, uv.z)));
     float len = len3(perp);
     v3 par = smul(-sqrtf(fabsf(1.0f - len * len)), n);
     return vadd(perp, par);
 }
 static inline float reflectance(float cosine, float ref_idx) { /* :166-171, pow(x,5) = x^4*x */
-    float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+    float r0 = divf(1.0f - ref_idx, 1.0f + ref_idx);
     r0 = r0 * r0;
     float x = 1.0f - cosine;
     float x2 = x * x;
-    return r0 + (1.0f - r0) * ((x2 * x2) * x);
+    return madd(1.0f - r0, (x2 * x2) * x, r0);
 }
 
 /* scatter: shader_sphere.wgsl:172-217 / shader_tris.wgsl:222-267 (metal: tris reflects the raw d) */
@@ -251,7 +283,7 @@ static ray_t scatter(const o_scene *sc, uint32_t *s, ray_t r, const hit_t *h) {
         v3 in = sc->mode == MODE_SPHERE ? norm3(r.d) : r.d;
         v3 refl = reflect3(in, h->n);
         v3 hemi = random_on_hemisphere(s, h->n, sc->eps);
-        out.d = norm3(vadd(refl, smul(fuzz, hemi)));
+        out.d = norm3(V(madd(fuzz, hemi.x, refl.x), madd(fuzz, hemi.y, refl.y), madd(fuzz, hemi.z, refl.z)));
     } else { /* MAT_DIELECTRIC and default */
         float ir = h->mat->params[0];
         if (h->front) ir = 1.0f / ir;
@@ -283,7 +315,8 @@ static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *cnt) {
         att = vmul(att, V(al[0] * 0.7f, al[1] * 0.7f, al[2] * 0.7f));
     }
     float tt = primary.d.y * 0.5f + 0.5f;
-    v3 sky = V(0.54f * (1.0f - tt) + 0.54f * tt, 0.86f * (1.0f - tt) + 0.7f * tt, 0.92f * (1.0f - tt) + 0.98f * tt);
+    v3 sky = V(madd(0.54f, tt, 0.54f * (1.0f - tt)), madd(0.7f, tt, 0.86f * (1.0f - tt)),
+               madd(0.98f, tt, 0.92f * (1.0f - tt)));
     return vmul(att, sky);
 }
 
@@ -291,14 +324,14 @@ static v3 trace(const o_scene *sc, ray_t primary, uint32_t *s, uint64_t *cnt) {
 static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, uint32_t y, uint32_t time,
                        uint64_t *cnt) {
     uint32_t s = (x * H + y) * time;
-    float aspect = (float)W / (float)H;
+    float aspect = divf((float)W, (float)H);
     float r1 = rng_float(&s), r2 = rng_float(&s);
-    float l = sqrtf(fmaf(r2, r2, r1 * r1));
-    float px = ((float)x + 0.5f) + r1 / l;
-    float py = ((float)y + 0.5f) + r2 / l;
-    float ux = px / ((float)W - 1.0f), uy = py / ((float)H - 1.0f);
-    ux = (2.0f * ux - 1.0f) * aspect;
-    uy = (2.0f * uy - 1.0f) * -1.0f;
+    float l = sqrtf(fmaf_c(r2, r2, r1 * r1));
+    float px = ((float)x + 0.5f) + (OC_RCPNORM ? r1 * (1.0f / l) : r1 / l);
+    float py = ((float)y + 0.5f) + (OC_RCPNORM ? r2 * (1.0f / l) : r2 / l);
+    float ux = divf(px, (float)W - 1.0f), uy = divf(py, (float)H - 1.0f);
+    ux = madd(2.0f, ux, -1.0f) * aspect;
+    uy = madd(2.0f, uy, -1.0f) * -1.0f;
     ray_t r = make_ray(sc, ux, uy, &s);
     v3 c = trace(sc, r, &s, cnt);
     return V(0.0f + c.x, 0.0f + c.y, 0.0f + c.z);
@@ -338,9 +371,9 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
                 uint32_t time = p->time0 + f * p->dtime;
                 v3 c = sample_pixel(&sc, p->width, p->height, x, y, time, q);
                 float w = 1.0f / (fminf((float)fc, (float)p->ema_cap) + 1.0f);
-                r = r * (1.0f - w) + c.x * w;
-                g = g * (1.0f - w) + c.y * w;
-                b = b * (1.0f - w) + c.z * w;
+                r = madd(c.x, w, r * (1.0f - w));
+                g = madd(c.y, w, g * (1.0f - w));
+                b = madd(c.z, w, b * (1.0f - w));
             }
             px[0] = r; px[1] = g; px[2] = b;
         }
