@@ -22,6 +22,7 @@
 #include "rt_device.hpp"
 
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 const char* hrt_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
@@ -128,9 +129,10 @@ struct rt_renderer {
     DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
-    DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused)
-    DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile done masks (2 words per tile), tile fold lock + cursor
-                                // (2), the free queue (1 per slot) and its tail (4); then the job -> slot map
+    DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
+    DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
+    DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
+                                // slot) and its tail (4); then the job -> slot map
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
 
@@ -141,12 +143,13 @@ struct rt_renderer {
     bool timing_pending = false;
     int last_variant = 0;
     std::vector<hipEvent_t> ev_trace;  // start/stop pairs around each k_trace launch of the last draw
-    uint32_t trace_pairs = 0;
+    uint32_t trace_pairs = 0, trace_pairs_pending = 0;
     uint32_t last_schedule = 0;
     uint32_t last_suspend = 0;
     uint32_t ring_slots = 0;  // fold-ring slots of the last sample-queue draw
     uint32_t ring_tiles = 0, ring_nchunks = 0;  // (diagnostics: HRT_RING_DUMP)
     size_t ring_ctl_words = 0;
+    uint64_t fold_bytes = 0;  // device memory of the last sample-queue draw's colour fold (rt_stats.fold_bytes)
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
@@ -461,6 +464,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 
     uint32_t launches = 0;
     if (schedule == RT_SCHEDULE_QUEUE) {
+        r->trace_pairs_pending = 0;
         P.tiles_w = (r->width + 7u) / 8u;
         P.tiles_h = (P.nrows + 7u) / 8u;
         const uint32_t ntiles = P.tiles_w * P.tiles_h;
@@ -473,48 +477,69 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.jf_log2 = 0;
         while ((2u << P.jf_log2) <= std::min(jf, 1024u)) P.jf_log2++;
         jf = 1u << P.jf_log2;
-        // frames per launch: at most 64 jobs per tile (the tile's done mask)
-        const uint32_t chunk = std::max(1u, std::min(count, 64u * jf));
-        const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
-        // fold ring: a power-of-two number of job slots (jf x 64 px x 16 B each) in the budget, at most one per
-        // job of a launch. A device short of memory gets a halved budget instead of a failed draw.
-        size_t budget = (size_t)std::min<uint32_t>(std::max<uint32_t>(r->params.queue_budget_mb, 1u), 2047u) << 20;
-        uint32_t log2s = 0;
-        auto plan = [&]() {
-            const size_t fit = std::max<size_t>(1, budget / ((size_t)jf << 10));
-            const uint64_t jobs = (uint64_t)ntiles * nchunks_max;
-            log2s = 0;
-            while ((2ull << log2s) <= fit && (1ull << log2s) < jobs && log2s < 20u) log2s++;
-            // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so jobs wait for their slot
-            static const char* cap_env = std::getenv("HRT_RING_SLOTS_MAX");
-            if (cap_env)
-                while (log2s > 0 && (1ull << log2s) > std::strtoull(cap_env, nullptr, 10)) log2s--;
-        };
-        plan();
-        const size_t zero_words = 4ull * ntiles + (4ull << log2s) + 4u;  // (log2s only shrinks below)
-        if (count) {
-            for (;;) {
-                rc = ensure(r->ring, ((size_t)jf << log2s) * 64u);
-                if (!rc) rc = ensure(r->ring_ctl, zero_words + (size_t)ntiles * nchunks_max);
-                if (rc != RT_ERR_ALLOC || budget <= ((size_t)jf << 10)) break;
+        // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a launch, then
+        // k_accumulate) when the budget holds at least min(count, 64) frames of colours, in launches of as many
+        // frames as it holds; else the fold ring in the budget (bounded memory, about 10 % slower: DESIGN.md §5).
+        size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
+        const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
+        P.ring_mode = budget / (frame_floats * 4u) < std::min<uint32_t>(std::max(count, 1u), 64u) ? 1u : 0u;
+        uint32_t chunk = 1, log2s = 0;
+        size_t zero_words = 0;
+        if (!P.ring_mode) {
+            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+            // a device short of memory gets smaller launches, down to one frame, instead of a failed draw
+            while (count && (rc = ensure(r->samples, (size_t)chunk * frame_floats)) == RT_ERR_ALLOC && chunk > 1u) {
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
-                budget /= 2u;
-                plan();
+                chunk = (chunk + 1u) / 2u;
             }
             if (rc) return rc;
+            P.samples = r->samples.ptr;
+            r->ring_slots = 0;
+            r->fold_bytes = (uint64_t)chunk * frame_floats * 4u;
+        } else {
+            // frames per launch: at most 48 jobs per tile (the done bits of the tile's fold word)
+            chunk = std::max(1u, std::min(count, 48u * jf));
+            const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
+            // a power-of-two number of job slots (jf x 64 px x 16 B each) in the budget, at most one per job of a
+            // launch; a device short of memory gets a halved budget instead of a failed draw
+            budget = std::min<size_t>(budget, 2047ull << 20);
+            auto plan = [&]() {
+                const size_t fit = std::max<size_t>(1, budget / ((size_t)jf << 10));
+                const uint64_t jobs = (uint64_t)ntiles * nchunks_max;
+                log2s = 0;
+                while ((2ull << log2s) <= fit && (1ull << log2s) < jobs && log2s < 20u) log2s++;
+                // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so jobs wait for their slot
+                static const char* cap_env = std::getenv("HRT_RING_SLOTS_MAX");
+                if (cap_env)
+                    while (log2s > 0 && (1ull << log2s) > std::strtoull(cap_env, nullptr, 10)) log2s--;
+            };
+            plan();
+            zero_words = 2ull * ntiles + (4ull << log2s) + 4u;  // (log2s only shrinks below)
+            if (count) {
+                for (;;) {
+                    rc = ensure(r->ring, ((size_t)jf << log2s) * 64u);
+                    if (!rc) rc = ensure(r->ring_ctl, zero_words + (size_t)ntiles * nchunks_max);
+                    if (rc != RT_ERR_ALLOC || budget <= ((size_t)jf << 10)) break;
+                    (void)hipGetLastError();
+                    budget /= 2u;
+                    plan();
+                }
+                if (rc) return rc;
+            }
+            P.ring = r->ring.ptr;
+            P.ring_log2 = log2s;
+            P.ring_bytes = (uint32_t)(((size_t)jf << log2s) * 1024u);
+            P.tile_fold = (unsigned long long*)r->ring_ctl.ptr;
+            P.ring_q = r->ring_ctl.ptr + 2ull * ntiles;
+            P.ring_tail = P.ring_q + (4u << log2s);
+            P.job_slot = r->ring_ctl.ptr + zero_words;
+            r->ring_slots = 1u << log2s;
+            r->ring_tiles = ntiles;
+            r->ring_ctl_words = zero_words + (size_t)ntiles * nchunks_max;
+            r->fold_bytes = (uint64_t)P.ring_bytes + 4ull * (4u * r->ring_slots + 4u) + 4ull * r->ring_ctl_words -
+                            4ull * zero_words + 8ull * ntiles;
         }
-        P.ring = r->ring.ptr;
-        P.ring_log2 = log2s;
-        P.ring_bytes = (uint32_t)(((size_t)jf << log2s) * 1024u);
-        P.tile_done = (unsigned long long*)r->ring_ctl.ptr;
-        P.tile_ctl = r->ring_ctl.ptr + 2ull * ntiles;
-        P.ring_q = r->ring_ctl.ptr + 4ull * ntiles;
-        P.ring_tail = P.ring_q + (4u << log2s);
-        P.job_slot = r->ring_ctl.ptr + zero_words;
         P.queue = r->counter.ptr + 15;
-        r->ring_slots = 1u << log2s;
-        r->ring_tiles = ntiles;
-        r->ring_ctl_words = zero_words + (size_t)ntiles * nchunks_max;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
         for (uint32_t done = 0; done < count; done += chunk) {
             P.nframes = std::min(chunk, count - done);
@@ -527,15 +552,21 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.njobs = (unsigned long long)ntiles * P.nchunks;
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
-            HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
-            rc = trace_events(r, launches);
+            if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
+            rc = trace_events(r, r->trace_pairs_pending);
             if (rc) return rc;
-            HIP_TRY(hipEventRecord(r->ev_trace[2 * launches], r->stream));
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
-            HIP_TRY(hipEventRecord(r->ev_trace[2 * launches + 1], r->stream));
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
+            r->trace_pairs_pending++;
             launches++;
+            if (!P.ring_mode) {
+                HIP_TRY(hrt_launch_accumulate(P, r->stream));
+                launches++;
+            }
         }
-        r->trace_pairs = launches;
+        r->trace_pairs = r->trace_pairs_pending;
+        r->trace_pairs_pending = 0;
     } else {
         const uint32_t fpl = std::max<uint32_t>(1u, r->params.frames_per_launch);
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
@@ -555,9 +586,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.launches = launches;
     r->stats.local_rows = P.nrows;
     std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
-    if (schedule == RT_SCHEDULE_QUEUE && count)
-        r->stats.ring_bytes = (uint64_t)P.ring_bytes + 4ull * (4u * r->ring_slots + 4u) +
-                              4ull * P.tiles_w * P.tiles_h * (4u + P.nchunks);
+    if (schedule == RT_SCHEDULE_QUEUE && count) {
+        r->stats.fold_ring = P.ring_mode;
+        r->stats.fold_bytes = r->fold_bytes;
+    }
     r->timing_pending = true;
     return RT_OK;
 }
@@ -632,7 +664,7 @@ int rt_device_count(void) {
 }
 
 const char* rt_build_info(void) {
-    return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_trace_split, k_trace_split_tris, k_trace, "
+    return "hrt gfx950 (HIP " HIP_VERSION_BUILD_NAME ") k_trace_split, k_trace_split_tris, k_trace, k_accumulate, "
            "k_render";
 }
 
@@ -658,7 +690,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.schedule = RT_SCHEDULE_AUTO;
     // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one chunk (one k_trace launch per draw, one launch
     // tail instead of six): C3 25.9 -> 26.1 Grays/s over 4 GiB
-    r->params.queue_budget_mb = 768;
+    r->params.queue_budget_mb = 32768;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
     r->params.job_frames = 0;  // per kernel (rt_draw_frames)

@@ -136,15 +136,18 @@ struct KParams {
     const MatDev* mats;
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
     unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
-    // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris): the fold ring. A job's samples go to a
-    // ring slot taken from a free queue when the job is dealt; each tile's jobs are folded into the image in
-    // order as they complete, and their slots return to the queue.
+    // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris). Two ways to fold the sample colours
+    // into the image in frame order: the sample buffer (ring_mode 0: every colour of the launch, folded by
+    // k_accumulate after it; fastest, memory O(frames x pixels)) or the fold ring (ring_mode 1: a job's samples go
+    // to a ring slot taken from a free queue when the job is dealt; each tile's jobs are folded in order inside
+    // the launch as they complete and their slots return to the queue; memory O(jobs in flight)).
+    float* samples;               // mode 0: nframes x (tiles_w * tiles_h) x 64 px x 3 colours, frame- then tile-major
+    uint32_t ring_mode, pad_m;
     float4* ring;                 // ring_jobs x job_frames x 64 px colour (r, g, b, unused)
     uint32_t* ring_q;             // [4 ring_jobs]: free queue: slot | (lap & 0x7FF) << 20 | valid << 31
     uint32_t* ring_tail;          // free-queue tickets issued (slots returned)
     uint32_t* job_slot;           // [tile * nchunks + chunk]: the job's slot (for its folder)
-    unsigned long long* tile_done;  // [tile]: bit c = the tile's job c has all its samples stored
-    uint32_t* tile_ctl;           // [tile]: fold lock, jobs folded (2 words)
+    unsigned long long* tile_fold;  // [tile]: bit c = job c stored (c < 48), bits 48-54 jobs folded, bit 63 lock
     uint32_t ring_log2;           // ring_jobs = 1 << ring_log2 (<= 2^20)
     uint32_t ring_bytes;          // size of `ring` (buffer-descriptor range)
     uint32_t jf_log2, pad_r;      // job_frames = 1 << jf_log2

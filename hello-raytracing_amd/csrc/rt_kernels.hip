@@ -912,67 +912,115 @@ __device__ __forceinline__ uint32_t ring_off(uint32_t slot, uint32_t fj, uint32_
     return (((slot << jf_log2) + fj) << 10) | (px << 4);
 }
 
-// Folds job `c` of tile `tile` (its frames, in order) into the image; the whole wave, lane = pixel. Then frees
-// the job's slot.
-__device__ __forceinline__ void fold_job(uint32_t tile, uint32_t c, uint32_t lane) {
+// Per-tile fold word (64 bits): bit c = job c has all its samples stored (c < 48), bits 48-54 = jobs folded
+// (the cursor), bit 63 = fold lock.
+constexpr unsigned long long TF_LOCK = 1ull << 63, TF_DONE = (1ull << 48) - 1ull;
+constexpr uint32_t TF_CURSOR_SHIFT = 48, TF_MAX_JOBS = 48;
+
+__device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
+    return ((unsigned long long)uniform(__shfl((uint32_t)(v >> 32), 0)) << 32) | uniform(__shfl((uint32_t)v, 0));
+}
+
+// The lock holder's fold session for `tile`, `v` the fold word it holds (locked, with its own job's bit): folds
+// the done jobs from the cursor on, in order, into the image (lane = pixel; the pixel's running value stays in
+// registers across the session's jobs), returns their slots to the free queue, then releases the lock with a
+// compare-and-swap that fails, and so folds on, if another job's bit arrived meanwhile.
+// U: frames loaded per round trip (registers: k_trace_split, at its 72-VGPR budget, folds with 1)
+template <uint32_t U>
+__device__ __forceinline__ void fold_session(uint32_t tile, unsigned long long v, uint32_t lane) {
     const KPtr K = kargs();
+    const uint32_t nc = K->nchunks;
     const uint32_t x = (tile % K->tiles_w) * 8u + (lane & 7u);
     const uint32_t kr = (tile / K->tiles_w) * 8u + (lane >> 3);
     const bool ok = x < K->W && kr < K->nrows;
     float* px = K->image + ((size_t)(ok ? kr : 0u) * K->W + (ok ? x : 0u)) * 3u;
+    unsigned long long* word = K->tile_fold + tile;
+    // the tile's job -> slot map, lane i holding job i's (written before each job's bit was set)
+    uint32_t slots = 0;
+    if (lane < nc) slots = __hip_atomic_load(K->job_slot + tile * nc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-    if (ok) {
-        a0 = __hip_atomic_load(px + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a1 = __hip_atomic_load(px + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a2 = __hip_atomic_load(px + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    bool loaded = false;
     const __amdgpu_buffer_rsrc_t rs = ring_rsrc();
-    uint32_t slot = 0;
-    if (lane == 0) slot = __hip_atomic_load(K->job_slot + tile * K->nchunks + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    slot = uniform(__shfl(slot, 0));
-    const uint32_t f0 = c << K->jf_log2, nf = min(1u << K->jf_log2, K->nframes - f0);
-    const uint32_t frame0 = K->frame0 + f0;
     const float cap = K->ema_cap;
-    uint32_t off = ring_off(slot, 0u, lane, K->jf_log2);
-    constexpr uint32_t U = 1;
-    uint32_t f = 0;
+    // v: the word as last seen in memory (locked by us; its cursor changes only when we release); p: jobs folded
+    uint32_t p = (uint32_t)(v >> TF_CURSOR_SHIFT) & 0x7Fu;
+#pragma nounroll
+    while (true) {
+        const uint32_t p0 = p;
+#pragma nounroll
+        while (p < nc && ((v >> p) & 1ull)) {
+            if (!loaded) {  // the pixel's value before this session (an earlier session or launch stored it)
+                if (ok) {
+                    a0 = __hip_atomic_load(px + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    a1 = __hip_atomic_load(px + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    a2 = __hip_atomic_load(px + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                loaded = true;
+            }
+            if (p >= 64u) break;  // (nc <= TF_MAX_JOBS: never)
+            const uint32_t slot = uniform(__shfl(slots, (int)p));
+            const uint32_t f0 = p << K->jf_log2, nf = min(1u << K->jf_log2, K->nframes - f0);
+            const uint32_t frame0 = K->frame0 + f0;
+            uint32_t off = ring_off(slot, 0u, lane, K->jf_log2);
+            uint32_t f = 0;
 #ifdef HRT_EXP_NOFOLD
-    f = nf;
+            f = nf;
 #endif
-    for (; f + U <= nf; f += U) {
-        u32x4 v[U];
+            for (; f + U <= nf; f += U) {
+                u32x4 c[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + (u << 10)), 0, 16);
+                for (uint32_t u = 0; u < U; u++) c[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + (u << 10)), 0, 16);
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const float w = 1.0f / (fmin_ieee((float)(frame0 + f + u), cap) + 1.0f);
-            const float omw = 1.0f - w;
-            a0 = a0 * omw + (0.0f + __uint_as_float(v[u].x)) * w;
-            a1 = a1 * omw + (0.0f + __uint_as_float(v[u].y)) * w;
-            a2 = a2 * omw + (0.0f + __uint_as_float(v[u].z)) * w;
+                for (uint32_t u = 0; u < U; u++) {
+                    const float w = 1.0f / (fmin_ieee((float)(frame0 + f + u), cap) + 1.0f);
+                    const float omw = 1.0f - w;
+                    a0 = a0 * omw + (0.0f + __uint_as_float(c[u].x)) * w;
+                    a1 = a1 * omw + (0.0f + __uint_as_float(c[u].y)) * w;
+                    a2 = a2 * omw + (0.0f + __uint_as_float(c[u].z)) * w;
+                }
+                off += U << 10;
+            }
+            for (; f < nf; f++, off += 1u << 10) {
+                const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
+                const float w = 1.0f / (fmin_ieee((float)(frame0 + f), cap) + 1.0f);
+                const float omw = 1.0f - w;
+                a0 = a0 * omw + (0.0f + __uint_as_float(c.x)) * w;
+                a1 = a1 * omw + (0.0f + __uint_as_float(c.y)) * w;
+                a2 = a2 * omw + (0.0f + __uint_as_float(c.z)) * w;
+            }
+            p++;
         }
-        off += U << 10;
-    }
-    for (; f < nf; f++, off += 1u << 10) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
-        const float w = 1.0f / (fmin_ieee((float)(frame0 + f), cap) + 1.0f);
-        const float omw = 1.0f - w;
-        a0 = a0 * omw + (0.0f + __uint_as_float(v.x)) * w;
-        a1 = a1 * omw + (0.0f + __uint_as_float(v.y)) * w;
-        a2 = a2 * omw + (0.0f + __uint_as_float(v.z)) * w;
-    }
-    if (ok) {
-        __hip_atomic_store(px + 0, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(px + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(px + 2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // every load of the slot has returned (its values are folded): return the slot to the free queue, for the
-    // job whose ticket is this return's + ring_jobs
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        const uint32_t m = __hip_atomic_fetch_add(K->ring_tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(K->ring_q + (m & ((4u << K->ring_log2) - 1u)), ring_q_entry(slot, m, K->ring_log2),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p > p0) {
+            if (ok) {
+                __hip_atomic_store(px + 0, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(px + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(px + 2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // the folded jobs' slots (their loads have returned: the values are in the sums) go back to the free
+            // queue, for the jobs whose tickets are these returns' + ring_jobs
+            uint32_t m = 0;
+            if (lane == 0) m = __hip_atomic_fetch_add(K->ring_tail, p - p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m = uniform(__shfl(m, 0));
+            const uint32_t k = lane;
+            const uint32_t slot = __shfl(slots, (int)((p0 + k) & 63u));  // (all lanes: the sources must be active)
+            if (k < p - p0)
+                __hip_atomic_store(K->ring_q + ((m + k) & ((4u << K->ring_log2) - 1u)),
+                                   ring_q_entry(slot, m + k, K->ring_log2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image stores before the release
+        }
+        const unsigned long long nv = (v & ~(TF_LOCK | (0x7Full << TF_CURSOR_SHIFT))) |
+                                      ((unsigned long long)p << TF_CURSOR_SHIFT);
+        unsigned long long r = v;
+        if (lane == 0) {
+            unsigned long long expect = v;
+            __hip_atomic_compare_exchange_strong(word, &expect, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            r = expect;  // the word's value before the exchange (== v on success)
+        }
+        r = bcast64(r);
+        if (r == v) return;
+        v = r;  // new bits arrived: fold on from p, with the slots of the jobs that just completed
+        if (lane < nc) slots = __hip_atomic_load(K->job_slot + tile * nc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -997,11 +1045,21 @@ struct WaveJobs {
     __device__ uint32_t cur() const { return (get(WJ_FLAGS) >> WJ_CUR_SHIFT) & 3u; }
 };
 
-// A dealt sample's job reference (`fl` in the kernels): its wave's entry and its frame within the job.
-__device__ __forceinline__ uint32_t sample_ref(uint32_t entry, uint32_t fj) { return (entry << 16) | fj; }
+// A dealt sample's job reference (`fl` in the kernels): with the fold ring its wave's entry and its frame within
+// the job; with the sample buffer its frame of the launch.
+__device__ __forceinline__ uint32_t sample_ref(const WaveJobs& J, uint32_t f0, uint32_t fj) {
+    return kargs()->ring_mode ? (J.cur() << 16) | fj : f0 + fj;
+}
 
 __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint32_t ref, const f3 c) {
     const KPtr K = kargs();
+    if (!K->ring_mode) {  // sample buffer: the colour at its frame of the launch, folded by k_accumulate
+        float* o = K->samples + ((size_t)ref * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
+        o[0] = c.x;
+        o[1] = c.y;
+        o[2] = c.z;
+        return;
+    }
     const uint32_t slot = J.w[WJ_SLOT + (ref >> 16)];  // per-lane entry: an LDS read, not a uniform value
     const uint32_t off = ring_off(slot, ref & 0xFFFFu, pix & 63u, K->jf_log2);
     const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
@@ -1048,44 +1106,20 @@ __device__ __forceinline__ bool idle_spin(const WaveJobs& J, uint32_t lane) {
     return true;
 }
 
-// One job of the wave is complete (every sample stored): mark it in the tile's done mask, then fold the tile as
-// far as its jobs are done if the fold lock is free (else its holder folds this job).
+// One job of the wave is complete (every sample stored): set its bit in the tile's fold word and, in the same
+// atomic, try the fold lock; the wave that gets it folds (fold_session), else the holder folds this job too.
+template <uint32_t U>
 __device__ __forceinline__ void job_complete(uint32_t tile, uint32_t c, uint32_t slot, uint32_t lane) {
     const KPtr K = kargs();
+    if (!K->ring_mode) return;  // sample buffer: k_accumulate folds after the launch
     if (lane == 0) __hip_atomic_store(K->job_slot + tile * K->nchunks + c, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores (and the slot) have reached memory
-    if (lane == 0) __hip_atomic_fetch_or(K->tile_done + tile, 1ull << c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the bit must be set before the lock is tried: a holder that releases after our failed try re-reads the mask
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t* lock = K->tile_ctl + 2u * tile;
-#pragma nounroll
-    while (true) {
-        uint32_t held = 0;
-        if (lane == 0) held = __hip_atomic_fetch_or(lock, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (uniform(__shfl(held, 0)) != 0u) return;  // the holder re-checks the mask after releasing
-        uint32_t p = 0;
-        unsigned long long m = 0;
-        if (lane == 0) {
-            p = __hip_atomic_load(lock + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            m = __hip_atomic_load(K->tile_done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        p = uniform(__shfl(p, 0));
-        m = ((unsigned long long)uniform(__shfl((uint32_t)(m >> 32), 0)) << 32) | uniform(__shfl((uint32_t)m, 0));
-        const uint32_t nc = K->nchunks;
-#pragma nounroll
-        while (p < nc && ((m >> p) & 1ull)) {
-            fold_job(tile, p, lane);
-            p++;
-        }
-        if (lane == 0) __hip_atomic_store(lock + 1, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image, slot and cursor stores before the release
-        if (lane == 0) __hip_atomic_store(lock, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p >= nc) return;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the release before the re-check
-        if (lane == 0) m = __hip_atomic_load(K->tile_done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t bit = (uint32_t)(m >> p) & 1u;
-        if (uniform(__shfl(bit, 0)) == 0u) return;  // job p not done yet: its wave folds it
-    }
+    unsigned long long old = 0;
+    if (lane == 0)
+        old = __hip_atomic_fetch_or(K->tile_fold + tile, (1ull << c) | TF_LOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = bcast64(old);
+    if (old & TF_LOCK) return;
+    fold_session<U>(tile, old | (1ull << c) | TF_LOCK, lane);
 }
 
 // The current job is dealt out (it completes in job_account once nothing of it is in flight).
@@ -1097,6 +1131,10 @@ __device__ __forceinline__ void job_close(const WaveJobs& J, uint32_t /*lane*/) 
 __device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uint32_t lane) {
     if (flags & WJ_SLOTTED) return true;
     const KPtr K = kargs();
+    if (!K->ring_mode) {  // sample buffer: no slot to wait for
+        J.set(WJ_FLAGS, flags | WJ_SLOTTED);
+        return true;
+    }
     const uint32_t cur = (flags >> WJ_CUR_SHIFT) & 3u;
     const uint32_t job = J.get(WJ_SLOT + cur);  // waiting: the job id is its free-queue ticket
     uint32_t slot = job;                        // the first ring_jobs jobs take the slots in order
@@ -1126,6 +1164,20 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
                                             uint32_t& job_f0, uint32_t& job_nf) {
     const KPtr K = kargs();
     uint32_t flags = J.get(WJ_FLAGS);
+    if (!K->ring_mode) {  // sample buffer: no entries, no slots
+        uint32_t j = 0;
+        if (lane == 0) j = (uint32_t)atomicAdd(K->queue, 1ull);
+        j = uniform(__shfl(j, 0));
+        if (j >= K->njobs) {
+            drained = true;
+            return false;
+        }
+        J.set(WJ_FLAGS, flags | WJ_DEALING);
+        job_tile = j / K->nchunks;
+        job_f0 = (j % K->nchunks) * K->job_frames;
+        job_nf = min(K->job_frames, K->nframes - job_f0);
+        return true;
+    }
     if (!(flags & WJ_WAITING)) {
         if ((flags & WJ_BUSY) == WJ_BUSY) {  // every entry still has samples in flight
             RINGSTAT_ADD(J, 0, 1);
@@ -1157,7 +1209,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
 
 // Samples just dealt from the current job (lanes that took one).
 __device__ __forceinline__ void job_dealt(const WaveJobs& J, uint32_t n) {
-    if (n == 0u) return;
+    if (n == 0u || !kargs()->ring_mode) return;
     J.set(WJ_IDLE, 0u);
     const uint32_t i = WJ_LIVE + ((J.get(WJ_FLAGS) >> WJ_CUR_SHIFT) & 3u);
     J.set(i, J.get(i) + n);
@@ -1166,7 +1218,9 @@ __device__ __forceinline__ void job_dealt(const WaveJobs& J, uint32_t n) {
 // End of a round: lanes whose sample finished (`fin`, colour stored) are counted off their jobs (the busy entry
 // whose tile and frames hold the sample); jobs neither current nor with anything in flight complete, and a job
 // that completes its tile folds it.
+template <uint32_t U = 2>
 __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_t ref, uint32_t lane) {
+    if (!kargs()->ring_mode) return;  // sample buffer: nothing to track
     const unsigned long long any = __ballot(fin);
     if (any != 0ull) {
         const uint32_t idx = ref >> 16;
@@ -1189,7 +1243,7 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
 #ifdef HRT_RINGSTAT
             const unsigned long long t0 = __builtin_readcyclecounter();
 #endif
-            job_complete(J.get(WJ_TILE + e), J.get(WJ_F0 + e) >> kargs()->jf_log2, J.get(WJ_SLOT + e), lane);
+            job_complete<U>(J.get(WJ_TILE + e), J.get(WJ_F0 + e) >> kargs()->jf_log2, J.get(WJ_SLOT + e), lane);
 #ifdef HRT_RINGSTAT
             RINGSTAT_ADD(J, 2, 1);
             RINGSTAT_ADD(J, 3, (__builtin_readcyclecounter() - t0) >> 4);
@@ -1249,7 +1303,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
                 ray.o = mk(ox, oy, oz);
                 ray.d = mk(dx, dy, dz);
                 s = ss;
-                fl = sample_ref(J.cur(), B.blk_f);
+                fl = sample_ref(J, B.job_f0, B.blk_f);
                 pix = B.job_tile * 64u + (uint32_t)src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
                 att = mk(1.0f, 1.0f, 1.0f);
@@ -1425,7 +1479,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // coherence: an incoherent sample queue measured 2.65x slower on C3), and one tile's frames are
 // spread over many waves. Each sample's colour goes to its tile's slot of the fold ring, and the wave that
 // completes a tile's last job folds the slot into the image in frame order per pixel with the reference's
-// mix (shader_sphere.wgsl:264-271; fold_job), so the image is bit-identical to k_render's and to
+// mix (shader_sphere.wgsl:264-271; fold_session), so the image is bit-identical to k_render's and to
 // count x rt_draw.
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
@@ -1487,7 +1541,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             if (need && rank < avail) {
                 const uint32_t sid = job_next + rank;
                 const uint32_t l = sid & 63u;
-                fl = sample_ref(J.cur(), sid >> 6);
+                fl = sample_ref(J, job_f0, sid >> 6);
                 pix = job_tile * 64u + l;
                 const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
                 const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
@@ -1648,7 +1702,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 ray.o = mk(b0.x, b0.y, b0.z);
                 ray.d = mk(b0.w, b1.x, b1.y);
                 s = __float_as_uint(b1.z);
-                fl = sample_ref(J.cur(), B.blk_f);
+                fl = sample_ref(J, B.job_f0, B.blk_f);
                 pix = B.job_tile * 64u + src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
                 att = mk(1.0f, 1.0f, 1.0f);
@@ -1754,7 +1808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     ray.o = mk(ox, oy, oz);
                     ray.d = mk(dx, dy, dz);
                     s = ss;
-                    fl = sample_ref(J.cur(), blk_f);
+                    fl = sample_ref(J, job_f0, blk_f);
                     pix = job_tile * 64u + (uint32_t)src;
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
@@ -1821,7 +1875,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             }
             qs = 0u;
         }
-        job_account(J, fin, fl, lane);
+        job_account<1>(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
     {
@@ -1962,6 +2016,39 @@ k_trace_split_tris(const KParams P) {
         for (int c = 0; c < 5; c++)
             if (sums[c]) atomicAdd(P.counter + c, sums[c]);
     }
+}
+
+// Sample buffer (ring_mode 0): folds P.nframes sample colours per pixel into the image, in frame order, with the
+// expression k_render uses (WGSL mix, shader_sphere.wgsl:264-271). One thread per tile-padded pixel, in the
+// buffer's tile-major order, so the frame-major colour reads are contiguous across the wave.
+__global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
+    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
+    const size_t q = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (q >= npad) return;
+    const uint32_t tile = (uint32_t)(q >> 6), l = (uint32_t)(q & 63u);
+    const uint32_t x = (tile % P.tiles_w) * 8u + (l & 7u);
+    const uint32_t kr = (tile / P.tiles_w) * 8u + (l >> 3);
+    if (x >= P.W || kr >= P.nrows) return;
+    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
+    float acc0 = px[0], acc1 = px[1], acc2 = px[2];
+    const float* c = P.samples + q * 3u;
+    for (uint32_t f = 0; f < P.nframes; f++, c += npad * 3u) {
+        const float w = 1.0f / (fmin_ieee((float)(P.frame0 + f), P.ema_cap) + 1.0f);
+        const float omw = 1.0f - w;
+        acc0 = acc0 * omw + (0.0f + c[0]) * w;
+        acc1 = acc1 * omw + (0.0f + c[1]) * w;
+        acc2 = acc2 * omw + (0.0f + c[2]) * w;
+    }
+    px[0] = acc0;
+    px[1] = acc1;
+    px[2] = acc2;
+}
+
+hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
+    const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
+    if (npad == 0 || P.nframes == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npad + 255u) / 256u)), dim3(256), 0, stream, P);
+    return hipGetLastError();
 }
 
 // Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE

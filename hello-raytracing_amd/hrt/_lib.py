@@ -62,7 +62,9 @@ class RtStats(C.Structure):
         ("trace_launches", C.c_uint32),
         ("suspend_below", C.c_uint32),
         ("kernel", C.c_char * 64),
-        ("ring_bytes", C.c_uint64),
+        ("fold_bytes", C.c_uint64),
+        ("fold_ring", C.c_uint32),
+        ("pad_stats", C.c_uint32),
     ]
 
 

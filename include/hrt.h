@@ -68,9 +68,12 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue fold-ring budget in MiB (slots, frames per launch); 768 */
-    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile); default 0 = per
-                                  kernel: 32 with the suspendable walks, 16 for the linear sphere scans */
+    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; 32768. The sample buffer when it holds
+                                  min(frames, 64) frames of colours (launches of as many frames as it holds),
+                                  else the fold ring in this budget (bounded memory, slower)             */
+    uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
+                                  power of two (at most 1024); default 0 = per kernel: 32 with the
+                                  suspendable walks, 16 for the linear sphere scans                      */
     uint32_t tri_bvh;          /* triangle program: 0 the reference's implicit-heap walk (default,
                                   parity), 1 opt-in binned-SAH tree with an ordered culling walk — the
                                   same closest hit except where the reference's 600-step cap or
@@ -106,8 +109,12 @@ typedef struct rt_stats {
                               0 = every query ran to completion (k_trace, k_render)                    */
     char kernel[64];       /* the ray-tracing kernel the last draw ran, as rocprofv3 names it without
                               "void " and the argument list, e.g. "k_trace_split<true>"                 */
-    uint64_t ring_bytes;   /* device memory of the sample queue's fold ring (slots x frames x 64 px x 16 B,
-                              plus 8 B of control per slot) in the last draw; 0 for the tiles schedule   */
+    uint64_t fold_bytes;   /* device memory the sample queue's colour fold used in the last draw: the sample
+                              buffer (frames per launch x pixels x 12 B) or the fold ring (job slots x
+                              job_frames x 64 px x 16 B plus control words); 0 for the tiles schedule    */
+    uint32_t fold_ring;    /* 1: the last draw folded through the fold ring (bounded memory), 0: through the
+                              sample buffer and k_accumulate (rt_params.queue_budget_mb decides)         */
+    uint32_t pad_stats;
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

@@ -15,7 +15,7 @@ import scenes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("configs", nargs="+")
-ap.add_argument("--budget", type=int, default=None)
+ap.add_argument("--budget", type=int, default=512)
 ap.add_argument("--jf", type=int, default=None)
 a = ap.parse_args()
 for cfg in a.configs:
@@ -31,6 +31,6 @@ for cfg in a.configs:
     st = r.stats()
     c = r.raw_counters(16)
     folds = max(c[7], 1)
-    print(f"{cfg}: {st.kernel_ms:.1f} ms kernel {st.kernel.decode()} ring {st.ring_bytes / 2**20:.0f} MiB "
+    print(f"{cfg}: {st.kernel_ms:.1f} ms kernel {st.kernel.decode()} fold {'ring' if st.fold_ring else 'buffer'} {st.fold_bytes / 2**20:.0f} MiB "
           f"launches {st.launches}: stall rounds {c[5]}, slot-wait rounds {c[6]}, folds {c[7]}, "
           f"fold {16 * c[8] / folds:.0f} cycles each ({16 * c[8] / 1e9:.2f} G wave-cycles)", flush=True)

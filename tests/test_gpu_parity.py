@@ -154,8 +154,10 @@ def test_auto_schedule_by_draw_size():
 
 
 def test_sample_queue_chunks_and_tris_mode():
-    """Fold rings smaller than the draw's jobs (1 and 2 MiB at 320x240: 32 and 64 job slots of 32 frames for
-    1200 jobs, so most jobs wait for their slot), and the triangle program under the queue schedule."""
+    """Budgets too small for the sample buffer: fold rings smaller than the draw's jobs (1 and 2 MiB at 320x240:
+    32 and 64 job slots of 32 frames for 1200 jobs, so most jobs wait for their slot); a budget holding 64+
+    frames: the sample buffer in launches of that many frames; and the triangle program under the queue
+    schedule."""
     sd = scenes.golden_scene("metal_materials", 320, 240)
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
@@ -165,9 +167,20 @@ def test_sample_queue_chunks_and_tris_mode():
         r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb)
         r.draw_frames(5, 1000, 10)
         st = r.stats()
-        ring = st.ring_bytes - 4 * 1200 * 5  # minus the per-tile fold words and job -> slot map
-        assert st.launches == 1 and (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), (st.launches, st.ring_bytes)
+        ring = st.fold_bytes - 4 * 1200 * 3  # minus the per-tile fold words and job -> slot map
+        assert st.fold_ring == 1 and st.launches == 1, (st.fold_ring, st.launches)
+        assert (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), st.fold_bytes
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
+    # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 64 MiB hold 72 frames -> launches of 72, 72, 56
+    ref = scenes.make_renderer(sd)
+    ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
+    ref.draw_frames(200, 1000, 10)
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=64)
+    r.draw_frames(200, 1000, 10)
+    st = r.stats()
+    assert st.fold_ring == 0 and st.launches == 6 and st.fold_bytes == 72 * 1200 * 64 * 12, (st.launches, st.fold_bytes)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     scene = hrt.SceneTris.new_suzane(96, 72)
     scene.init()
     sd = scenes.SceneDef("suzane", hrt.RT_MODE_TRIS, 96, 72, scene.camera, bvh=scene.tris_bvh.view(), frames=4)
@@ -182,7 +195,7 @@ def test_sample_queue_chunks_and_tris_mode():
     assert_parity(imgs[1], ref_img, "suzane tris, queue schedule")
 
 
-def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, out_name: str):
+def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, out_name: str, budget_mb: int = 0):
     """Renders `scene_expr` (a scenes.* SceneDef) under the queue schedule in a child process with extra
     environment (the fault-injection and slot-cap knobs are read once per process); returns (image, stats)."""
     import json
@@ -193,9 +206,11 @@ def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, o
 
     code = ("import sys, json; sys.path[:0] = ['hello-raytracing_amd', 'tests']; import numpy as np, scenes, hrt\n"
             f"sd = {scene_expr}; r = scenes.make_renderer(sd)\n"
-            f"r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE); r.draw_frames({frames}, 1000, 10)\n"
+            f"r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE{f', queue_budget_mb={budget_mb}' if budget_mb else ''}); "
+            f"r.draw_frames({frames}, 1000, 10)\n"
             "np.save(sys.argv[1], r.read_image()); st = r.stats()\n"
-            "print(json.dumps({'launches': st.launches, 'ring_bytes': st.ring_bytes, 'queries': st.queries}))\n")
+            "print(json.dumps({'launches': st.launches, 'fold_bytes': st.fold_bytes, 'fold_ring': st.fold_ring, "
+            "'queries': st.queries}))\n")
     root = Path(__file__).resolve().parents[1]
     out = root / "tests" / "output"
     out.mkdir(exist_ok=True)
@@ -205,19 +220,24 @@ def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, o
     return np.load(out / out_name), json.loads(p.stdout.strip().splitlines()[-1])
 
 
-def test_fold_ring_allocation_failure_halves_the_budget():
-    """A fold-ring allocation the device refuses (fault injection: every allocation above 100 MiB fails in a
-    subprocess with HRT_FAIL_ALLOC_ABOVE_MB=100): the renderer halves its budget (fewer slots) until the ring
-    fits and the draw completes, bit-identical to the default draw."""
-    small, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"},
-                                            "scenes.golden_scene('metal_materials', 512, 512)", 40, "alloc_small.npy")
-    assert 0 < st["ring_bytes"] <= 100 << 20, st  # 16384 slots x 16 KB = 256 MiB do not fit: 4096 slots
+def test_fold_allocation_failure_shrinks_the_launches():
+    """Allocations the device refuses (fault injection: every allocation above 100 MiB fails in a subprocess
+    with HRT_FAIL_ALLOC_ABOVE_MB=100): the sample buffer (512x512 x 100 frames = 315 MB) is halved until it
+    fits (launches of 25 frames); with a 160 MiB budget (under 64 frames of colours) the fold ring (4096 slots
+    x 32 KB) halves its budget until it fits. Both bit-identical to the default draw."""
+    expr = "scenes.golden_scene('metal_materials', 512, 512)"
+    small, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"}, expr, 100, "alloc_small.npy")
+    assert st["fold_ring"] == 0 and st["launches"] == 8 and 0 < st["fold_bytes"] <= 100 << 20, st
+    ring, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"}, expr, 100, "alloc_ring.npy",
+                                           budget_mb=160)
+    assert st["fold_ring"] == 1 and 0 < st["fold_bytes"] <= 100 << 20, st
     sd = scenes.golden_scene("metal_materials", 512, 512)
     r = scenes.make_renderer(sd)
     r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE)
-    r.draw_frames(40, 1000, 10)
-    assert r.stats().launches == 1 and r.stats().ring_bytes > 100 << 20
+    r.draw_frames(100, 1000, 10)
+    assert r.stats().launches == 2 and r.stats().fold_bytes > 100 << 20
     np.testing.assert_array_equal(small.view(np.uint32), r.read_image().view(np.uint32))
+    np.testing.assert_array_equal(ring.view(np.uint32), r.read_image().view(np.uint32))
 
 
 @pytest.mark.parametrize("slots", [1, 2, 8])
@@ -227,8 +247,9 @@ def test_fold_ring_slot_reuse_bit_identical(slots):
     64 frames (two jobs per tile), and C2 (k_trace, four): images bit-identical to the tiles schedule, same
     ray counts."""
     for expr in ("scenes.config_c3(160, 96, 64)", "scenes.config_c4(160, 96, 64)", "scenes.config_c2(160, 96, 64)"):
-        img, st = _queue_render_in_subprocess({"HRT_RING_SLOTS_MAX": str(slots)}, expr, 64, f"ring_{slots}.npy")
-        assert st["launches"] == 1 and st["ring_bytes"] <= slots * (32 << 10) + (16 << 10), st
+        img, st = _queue_render_in_subprocess({"HRT_RING_SLOTS_MAX": str(slots)}, expr, 64, f"ring_{slots}.npy",
+                                              budget_mb=1)
+        assert st["fold_ring"] == 1 and st["launches"] == 1 and st["fold_bytes"] <= slots * (32 << 10) + (16 << 10), st
         sd = eval(expr)
         r = scenes.make_renderer(sd)
         r.set_params(schedule=hrt.RT_SCHEDULE_TILES)
