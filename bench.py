@@ -364,8 +364,9 @@ def main() -> int:
                                     + tri_flop) / nl
         executed = executed_flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
         px = local_rows * sd.width
-        if schedule == 2:  # k_trace writes one 12 B colour per sample; the sphere arrays are read once
-            alg_bytes = 12.0 * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
+        if schedule == 2:  # one colour per sample (12 B; 16 B through the fold ring); the spheres read once
+            per_sample = 16.0 if st_last.fold_ring else 12.0
+            alg_bytes = per_sample * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
         else:  # k_render reads and writes the framebuffer once per launch
             alg_bytes = 24.0 * px + 64.0 * nslots
         kernel_sym = st_last.kernel.decode() if st_last is not None else ""
@@ -398,6 +399,10 @@ def main() -> int:
                 "rays_per_step": round(total_q / args.steps),
                 "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
                 "parallelism": f"rows{world}",
+                # how the sample queue folded the colours in frame order (rt_params.queue_budget_mb):
+                # "sample-buffer" (+ k_accumulate) or the bounded-memory "fold-ring"; device bytes it used
+                "fold": ("fold-ring" if st_last.fold_ring else "sample-buffer") if schedule == 2 else "in-register",
+                "fold_bytes": int(st_last.fold_bytes) if schedule == 2 else 0,
             },
             # The path is FP32-VALU issue bound (no MFMA: no dense contraction; HBM ~2 % busy). `achieved` =
             # the FP32 FLOPs the kernel executes (its exact in-kernel test counters x FLOP per test, + the

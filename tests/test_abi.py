@@ -59,7 +59,7 @@ def test_struct_layouts_match_header():
         assert [f for f, _ in fields] == [f for f, _ in got], name
         assert [C.sizeof(t) for _, t in fields] == [C.sizeof(t) for _, t in got], name
     assert C.sizeof(hrt.RtParams) == 12 * 4
-    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64
+    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64 + 8 + 4 + 4
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
 
