@@ -229,6 +229,19 @@ __device__ __forceinline__ f3 normalize_rng(f3 a) {
     return mk(div_rn_mid(a.x, d), div_rn_mid(a.y, d), div_rn_mid(a.z, d));
 }
 
+// normalize() of any vector: the sequences above when every component's magnitude lies in [2^-40, 2^40] (then
+// dot is in [2^-80, 3 x 2^80] and the length and quotients inside their ranges), else the IEEE operations;
+// bit-identical to normalize() either way (GPU self-check: rt_check_exact_math).
+__device__ __forceinline__ f3 normalize_exact(f3 a) {
+    const float lo = fmin_ieee(fmin_ieee(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    const float hi = fmax_ieee(fmax_ieee(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    if (lo >= 0x1p-40f && hi <= 0x1p40f) {
+        const RcpRN d = rcp_rn_setup(sqrt_rn_mid(dot(a, a)));
+        return mk(div_rn_mid(a.x, d), div_rn_mid(a.y, d), div_rn_mid(a.z, d));
+    }
+    return normalize(a);
+}
+
 // PCG hash step — shader_sphere.wgsl:87-93.
 __device__ __forceinline__ uint32_t pcg_next(uint32_t s) {
     uint32_t old = s + 747796405u + 2891336453u;

@@ -781,7 +781,7 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
     if (lambert || metal) hemi = random_on_hemisphere<MODE>(s, h.n);  // 3 draws, both arms
     f3 u = hemi;
     if (metal) {
-        const f3 in = MODE == MODE_SPHERE ? normalize(r.d) : r.d;
+        const f3 in = MODE == MODE_SPHERE ? normalize_exact(r.d) : r.d;
         u = reflect(in, h.n) + h.param * hemi;
     } else if (!lambert) {  // MAT_DIELECTRIC and the default arm
         // ir = front ? 1 / param : param, and reflectance's r0 * r0 for that ir, from the host (DielConsts)
@@ -798,7 +798,8 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
         u = refl ? reflect(r.d, h.n) : refract(r.d, h.n, ir);
     }
     r.o = h.p;
-    r.d = lambert ? hemi : normalize(u);
+    // (the triangle / mixed kernels keep the IEEE form: the fast one costs them spills)
+    r.d = lambert ? hemi : (MODE == MODE_SPHERE ? normalize_exact(u) : normalize(u));
 }
 
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
@@ -1999,7 +2000,7 @@ k_trace_split_tris(const KParams P) {
             }
             qs = 0u;
         }
-        job_account(J, fin, fl, lane);
+        job_account<SCAN == SCAN_BVH ? 1 : 2>(J, fin, fl, lane);
     }
 #ifdef HRT_RINGSTAT
     if (lane == 0)
@@ -2053,7 +2054,8 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 
 // Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE
 // operations (correctly rounded in this build): n random cases per test, counted mismatches in out[0..2]:
-// [0] normalize_rng vs normalize on vectors of rng floats (the hemisphere sample), [1] div_rn_mid vs `/` on
+// [0] normalize_rng vs normalize on vectors of rng floats (the hemisphere sample) and normalize_exact vs
+// normalize on signed vectors (magnitudes 2^-48 .. 2^48), [1] div_rn_mid vs `/` on
 // log-uniform operands in [2^-60, 2^60] (random signs, and x = 0), [2] sqrt_rn_mid vs sqrtf on [2^-100, 2^100].
 __global__ __launch_bounds__(256) void k_check_exact_math(unsigned long long n, uint32_t seed,
                                                           unsigned long long* out) {
@@ -2066,6 +2068,21 @@ __global__ __launch_bounds__(256) void k_check_exact_math(unsigned long long n, 
         if (__float_as_uint(a.x) != __float_as_uint(b.x) || __float_as_uint(a.y) != __float_as_uint(b.y) ||
             __float_as_uint(a.z) != __float_as_uint(b.z))
             bad[0]++;
+        // normalize_exact on signed vectors with component magnitudes 2^-48 .. 2^48 (some outside its fast range)
+        {
+            uint32_t t = pcg_next(s ^ 0x9E3779B9u);
+            float w[3];
+            for (int k = 0; k < 3; k++) {
+                t = pcg_next(t);
+                const uint32_t e = 127u - 48u + (t % 97u);
+                w[k] = __uint_as_float((e << 23) | (pcg_next(t) & 0x7FFFFFu) | (t & 0x80000000u));
+            }
+            const f3 g = mk(w[0], w[1], w[2]);
+            const f3 ga = normalize(g), gb = normalize_exact(g);
+            if (__float_as_uint(ga.x) != __float_as_uint(gb.x) || __float_as_uint(ga.y) != __float_as_uint(gb.y) ||
+                __float_as_uint(ga.z) != __float_as_uint(gb.z))
+                bad[0]++;
+        }
         // log-uniform magnitudes: exponent in [-60, 60), random mantissa and sign
         s = pcg_next(s);
         const uint32_t ex = 67u + (s % 120u), ey = 67u + ((s >> 8) % 120u);
