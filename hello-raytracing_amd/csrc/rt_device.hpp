@@ -229,6 +229,16 @@ __device__ __forceinline__ f3 normalize_rng(f3 a) {
     return mk(div_rn_mid(a.x, d), div_rn_mid(a.y, d), div_rn_mid(a.z, d));
 }
 
+// sqrt / division with the sequences above where their ranges hold, else the IEEE operation; bit-identical.
+__device__ __forceinline__ float sqrt_exact(float x) {
+    return (x >= 0x1p-100f && x <= 0x1p100f) ? sqrt_rn_mid(x) : __builtin_sqrtf(x);
+}
+__device__ __forceinline__ float div_exact(float x, float l) {
+    const float ax = __builtin_fabsf(x), al = __builtin_fabsf(l);
+    if (ax >= 0x1p-60f && ax <= 0x1p60f && al >= 0x1p-60f && al <= 0x1p60f) return div_rn_mid(x, rcp_rn_setup(l));
+    return x / l;
+}
+
 // normalize() of any vector: the sequences above when every component's magnitude lies in [2^-40, 2^40] (then
 // dot is in [2^-80, 3 x 2^80] and the length and quotients inside their ranges), else the IEEE operations;
 // bit-identical to normalize() either way (GPU self-check: rt_check_exact_math).
@@ -259,8 +269,8 @@ __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - (2.0f * dot(v, n)
 __device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {
     float cos_t = fmin_ieee(dot(-uv, n), 1.0f);
     f3 perp = e * (uv + cos_t * n);
-    float len = length(perp);
-    f3 par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len * len))) * n;
+    float len = sqrt_exact(dot(perp, perp));
+    f3 par = (-sqrt_exact(__builtin_fabsf(1.0f - len * len))) * n;
     return perp + par;
 }
 __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {

@@ -187,7 +187,7 @@ __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
     const float disc = __builtin_fmaf(b, b, (-a4) * c);
     if (!(disc >= 0.0f && b <= 0.0f)) return -1.0f;  // t would be <= 0, NaN or -1: never accepted
-    return (-b - __builtin_sqrtf(disc)) / a2;
+    return div_exact(-b - sqrt_exact(disc), a2);
 }
 
 #ifndef HRT_SLAB_FMA
@@ -789,7 +789,7 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
                                                                                      : &P.mats[h.id >> 3].inv_param;
         const float ir = h.front ? dc[0] : h.param;
         const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
-        const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        const float sin_t = sqrt_exact(1.0f - cos_t * cos_t);
         bool refl = ir * sin_t > 1.0f;  // cannot_refract; WGSL || short-circuits the RNG draw
         if (!refl) {
             const float f = rng_float(s);
