@@ -266,11 +266,14 @@ __device__ __forceinline__ float rng_float(uint32_t& s) {
 
 // reflect / refract / reflectance — shader_sphere.wgsl:156-171.
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - (2.0f * dot(v, n)) * n; }
+// FAST: the range-guarded exact square roots (sphere program); else the IEEE ones (the same bits).
+template <bool FAST = true>
 __device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {
     float cos_t = fmin_ieee(dot(-uv, n), 1.0f);
     f3 perp = e * (uv + cos_t * n);
-    float len = sqrt_exact(dot(perp, perp));
-    f3 par = (-sqrt_exact(__builtin_fabsf(1.0f - len * len))) * n;
+    float len = FAST ? sqrt_exact(dot(perp, perp)) : length(perp);
+    const float q = __builtin_fabsf(1.0f - len * len);
+    f3 par = (-(FAST ? sqrt_exact(q) : __builtin_sqrtf(q))) * n;
     return perp + par;
 }
 __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {

@@ -180,6 +180,8 @@ __device__ __forceinline__ bool beats(float t, int i, float bt, int bi) {
 }
 
 // The reference's t for a sphere given its (cx, cy, cz, r*r) — same ops as exact_sphere_t.
+// FAST: the range-guarded exact sqrt / division (the sphere program's split kernel); else IEEE (same bits).
+template <bool FAST = false>
 __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float a4, float a2) {
     const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
     const float bd = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
@@ -187,7 +189,8 @@ __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
     const float disc = __builtin_fmaf(b, b, (-a4) * c);
     if (!(disc >= 0.0f && b <= 0.0f)) return -1.0f;  // t would be <= 0, NaN or -1: never accepted
-    return div_exact(-b - sqrt_exact(disc), a2);
+    if (FAST) return div_exact(-b - sqrt_exact(disc), a2);
+    return (-b - __builtin_sqrtf(disc)) / a2;
 }
 
 #ifndef HRT_SLAB_FMA
@@ -271,7 +274,7 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 }
 
 // Returns true when the walk has to run (false: bvh_end does the full scan).
-template <bool H16 = false>
+template <bool H16 = false, bool FAST = false>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -292,7 +295,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     int bc = -1;
     for (uint32_t k = 0; k < P.nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
-        const float t = exact_t_geo(P.sph_geo[i], r, a4, a2);
+        const float t = exact_t_geo<FAST>(P.sph_geo[i], r, a4, a2);
         if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
     tally.spheres += P.nlarge;
@@ -409,7 +412,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #endif
             const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
             for (uint32_t j = 0; j < cnt; j++) {
-                const float t = exact_t_geo(P.bvh_sph[first + j], r, a4, a2);
+                const float t = exact_t_geo<SELECT>(P.bvh_sph[first + j], r, a4, a2);
                 if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
                     if (t < bt || (bc >= 0 && P.bvh_slot[first + j] < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                 }
@@ -789,13 +792,13 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
                                                                                      : &P.mats[h.id >> 3].inv_param;
         const float ir = h.front ? dc[0] : h.param;
         const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
-        const float sin_t = sqrt_exact(1.0f - cos_t * cos_t);
+        const float sin_t = MODE == MODE_SPHERE ? sqrt_exact(1.0f - cos_t * cos_t) : __builtin_sqrtf(1.0f - cos_t * cos_t);
         bool refl = ir * sin_t > 1.0f;  // cannot_refract; WGSL || short-circuits the RNG draw
         if (!refl) {
             const float f = rng_float(s);
             refl = reflectance_r0sq(cos_t, h.front ? dc[1] : dc[2]) > (f - __builtin_floorf(f));
         }
-        u = refl ? reflect(r.d, h.n) : refract(r.d, h.n, ir);
+        u = refl ? reflect(r.d, h.n) : refract<MODE == MODE_SPHERE>(r.d, h.n, ir);
     }
     r.o = h.p;
     // (the triangle / mixed kernels keep the IEEE form: the fast one costs them spills)
@@ -1834,7 +1837,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #endif
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
-                qs = bvh_begin<true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+                qs = bvh_begin<true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
             } else {  // bounce cap 0: the sample is the sky colour
                 qs = 3u;
             }
