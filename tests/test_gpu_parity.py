@@ -76,6 +76,12 @@ def test_golden_scene_full_draw_sample_queue(name):
     st = r.stats()
     assert st.schedule == hrt.RT_SCHEDULE_QUEUE and st.suspend_below > 0 and st.variant == 4
     np.testing.assert_array_equal(r.read_image().view(np.uint32), per_frame.view(np.uint32))
+    # the fold ring (a 16 MiB budget: 512 slots of 32 frames for 4096 tiles x 4 jobs) gives the same bits
+    r = scenes.make_renderer(sd)
+    r.set_params(queue_budget_mb=16)
+    r.draw_frames(scenes.GOLDEN_FRAMES, 1000, 10)
+    assert r.stats().fold_ring == 1
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), per_frame.view(np.uint32))
 
 
 @pytest.mark.parametrize("schedule", [1, 2])
@@ -461,14 +467,14 @@ def test_full_size_headline_configs_agree():
 def test_hip_reproduces_oracle_fixtures(name):
     """The committed oracle outputs (tests/golden/oracle) re-rendered on the GPU through the C-ABI with the
     same row subset: image bits, ray counts and triangle-program work counts, under the auto schedule and
-    the sample queue (suspendable walks)."""
+    the sample queue (suspendable walks), folded through the sample buffer and through the fold ring."""
     sd, (row0, step) = scenes.oracle_fixture_cases()[name]
     want, man = scenes.load_oracle_fixture(name)
-    for schedule in (hrt.RT_SCHEDULE_AUTO, hrt.RT_SCHEDULE_QUEUE):
+    for schedule, budget in ((hrt.RT_SCHEDULE_AUTO, 0), (hrt.RT_SCHEDULE_QUEUE, 0), (hrt.RT_SCHEDULE_QUEUE, 1)):
         r = scenes.make_renderer(sd)
-        r.set_params(row0=row0, row_step=step, schedule=schedule)
+        r.set_params(row0=row0, row_step=step, schedule=schedule, **({"queue_budget_mb": budget} if budget else {}))
         r.draw_frames(sd.frames, 1000, 10)
-        assert_parity(r.read_image(), want, f"{name} schedule {schedule}")
+        assert_parity(r.read_image(), want, f"{name} schedule {schedule} budget {budget}")
         st = r.stats()
         assert st.queries == man["queries"]
         assert (st.node_tests, st.tri_tests) == (man["node_tests"], man["tri_tests"])  # heap-walk work
