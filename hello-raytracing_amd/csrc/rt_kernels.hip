@@ -1737,6 +1737,9 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
 // LNODES (small trees: <= LNODE_CAP nodes, depth <= 8): the fp16 nodes are copied into LDS once per
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
+#ifndef HRT_DEFER_DIELECTRIC
+#define HRT_DEFER_DIELECTRIC 0  // k_trace_split: dielectric hits wait for this many in the wave (0: off)
+#endif
 template <bool LNODES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
@@ -1850,34 +1853,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     qs = 2u;
             }
         }
+#if HRT_DEFER_DIELECTRIC
+        const bool walkers = __ballot(have && qs == 1u) != 0ull;
+#endif
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
             tally.lshade++;
             if (first_active_lane()) tally.wshade++;
 #endif
-            bool done = true;
-            if (qs == 2u) {
+            bool done = true, defer = false;
+            if ((qs & 15u) == 2u) {  // (qs >> 4: rounds this lane's shading has waited)
                 float best = FLT_MAX_REF;
                 const int bi = bvh_end(P, ray, Q, best, tally);
-                queries++;
-                if (bi >= 0) {
-                    Hit h;
-                    sphere_record(P, ray, bi, best, h);
-                    scatter<MODE>(P, s, ray, h);
-                    att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
-                    bounce++;
-                    done = bounce >= P.bounces;
+#if HRT_DEFER_DIELECTRIC
+                // a dielectric hit waits (a few rounds at most, and only while lanes still walk) until several
+                // lanes of the wave have one, so the dielectric arm of scatter runs for them together; the
+                // lane's own arithmetic is unchanged (bvh_end is pure when the walk did not fall back)
+                const bool diel = bi >= 0 && Q.full_scan == 0u && P.sph_aux[bi].id != 1u && P.sph_aux[bi].id != 2u;
+                const uint32_t nd = (uint32_t)__popcll(__ballot(diel));
+                defer = diel && walkers && nd < HRT_DEFER_DIELECTRIC && (qs >> 4) < 3u;
+#endif
+                if (!defer) {
+                    queries++;
+                    if (bi >= 0) {
+                        Hit h;
+                        sphere_record(P, ray, bi, best, h);
+                        scatter<MODE>(P, s, ray, h);
+                        att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                        bounce++;
+                        done = bounce >= P.bounces;
+                    }
                 }
             }
-            if (done) {
-                const float u = 1.0f - sky_t;
-                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
-                const f3 c = att * sky;
-                ring_store(J, pix, fl, c);
-                have = false;
-                fin = true;
+            if (defer) {
+                qs += 16u;
+            } else {
+                if (done) {
+                    const float u = 1.0f - sky_t;
+                    const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+                    const f3 c = att * sky;
+                    ring_store(J, pix, fl, c);
+                    have = false;
+                    fin = true;
+                }
+                qs = 0u;
             }
-            qs = 0u;
         }
         job_account<1>(J, fin, fl, lane);
     }
