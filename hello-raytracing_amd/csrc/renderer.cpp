@@ -902,6 +902,19 @@ int rt_synchronize(rt_renderer* r) {
     return finish_stats(r);
 }
 
+int rt_release_scratch(rt_renderer* r) {
+    if (!r) return fail(RT_ERR_ARG, "rt_release_scratch: null");
+    if (r->timing_pending) {
+        const int rc = finish_stats(r);  // the pending draws' counters, and their kernels done
+        if (rc) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    r->samples.release();
+    r->ring.release();
+    r->ring_ctl.release();
+    return RT_OK;
+}
+
 int rt_get_stats(const rt_renderer* r, rt_stats* out) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_get_stats: null");
     int rc = finish_stats(const_cast<rt_renderer*>(r));

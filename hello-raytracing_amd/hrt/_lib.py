@@ -92,6 +92,7 @@ SIGNATURES = {
     "rt_reset_frame_count": (C.c_int, [_P]),
     "rt_resize": (C.c_int, [_P, _U32, _U32]),
     "rt_synchronize": (C.c_int, [_P]),
+    "rt_release_scratch": (C.c_int, [_P]),
     "rt_get_stats": (C.c_int, [_P, C.POINTER(RtStats)]),
     "rt_get_raw_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "rt_diagnostic_build": (C.c_int, []),

@@ -304,6 +304,10 @@ class Renderer:
         check(lib().rt_resize(self._h, width, height), "resize")
         self.width, self.height = max(1, width), max(1, height)
 
+    def release_scratch(self) -> None:
+        """Free the sample queue's colour-fold memory (include/hrt.h rt_release_scratch)."""
+        check(lib().rt_release_scratch(self._h), "release_scratch")
+
     def synchronize(self) -> None:
         check(lib().rt_synchronize(self._h), "synchronize")
 

@@ -159,6 +159,11 @@ int rt_reset_frame_count(rt_renderer *r);
 int rt_resize(rt_renderer *r, uint32_t width, uint32_t height);
 int rt_synchronize(rt_renderer *r);
 int rt_get_stats(const rt_renderer *r, rt_stats *out);
+/* Frees the sample queue's colour-fold memory (the sample buffer or the fold ring, rt_stats.fold_bytes)
+ * after the pending draws; the next queue draw allocates it again. For a renderer kept alive between
+ * renders beside other work: the 32 GiB default budget lets one C3 render hold 25.5 GB (no reference
+ * counterpart: wgpu frees nothing either, but the reference has no per-sample buffer). */
+int rt_release_scratch(rt_renderer *r);
 
 /* Raw per-draw device counters (no reference counterpart; diagnostics). Slots 0-4 are the rt_stats
  * work counters; in the diagnostic build (rt_diagnostic_build() == 1, lib/libhrt_diag.so) slots 8-11
@@ -174,7 +179,8 @@ int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 
 /* Self-check of the kernels' range-restricted correctly rounded sqrt / division sequences against the IEEE
  * operations on n random cases each (diagnostics): mismatches[0] normalize of rng
- * vectors, [1] division on [2^-60, 2^60], [2] sqrt on [2^-100, 2^100]. All three must be 0. */
+ * vectors and normalize_exact of signed vectors, [1] division on [2^-60, 2^60], [2] sqrt on [2^-100, 2^100].
+ * All three must be 0. */
 int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]);
 
 /* Thread-local message for the last failing call. */

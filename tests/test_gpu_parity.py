@@ -246,6 +246,24 @@ def test_fold_allocation_failure_shrinks_the_launches():
     np.testing.assert_array_equal(ring.view(np.uint32), r.read_image().view(np.uint32))
 
 
+@pytest.mark.parametrize("budget_mb", [0, 1])
+def test_release_scratch_then_draw_again(budget_mb):
+    """rt_release_scratch frees the colour-fold memory (sample buffer, or the fold ring with a 1 MiB budget);
+    the next draw allocates it again and renders the same bits."""
+    sd = scenes.config_c3(160, 96, 64)
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **({"queue_budget_mb": budget_mb} if budget_mb else {}))
+    r.draw_frames(sd.frames, 1000, 10)
+    first = r.read_image()
+    assert r.stats().fold_bytes > 0 and r.stats().fold_ring == (1 if budget_mb else 0)
+    r.release_scratch()
+    r.reset_frame_count()
+    r.draw_frames(sd.frames, 1000, 10)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), first.view(np.uint32))
+    r.release_scratch()
+    r.release_scratch()  # idempotent
+
+
 @pytest.mark.parametrize("slots", [1, 2, 8])
 def test_fold_ring_slot_reuse_bit_identical(slots):
     """Very few fold-ring slots (HRT_RING_SLOTS_MAX): nearly every job waits in the free queue for a slot to

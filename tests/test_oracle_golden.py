@@ -5,7 +5,8 @@ tests/golden/make_fixtures.py; scene definitions restate tests/rendering_tests.r
 rendered with 100 frames at time 1000 + 10 i, on an unknown GPU whose float behaviour
 (FMA contraction, sqrt/pow/tan precision) cannot be reproduced, so the bar is statistical:
   * the reference harness's own metric: mean |du8| <= 2 % of 255 (rendering_tests.rs:11, :84-131) — all 7;
-  * non-glass scenes: >= 99.9 % of u8 channels bit-exact, max |du8| <= 6;
+  * non-glass scenes: >= 99.98 % of u8 channels bit-exact, max |du8| <= 5 — the float-noise floor the
+    contract study shows irreducible by any of six float contracts (DESIGN.md §2, test_contract_study.py);
   * glass scenes (dielectric_materials, complex_scene): mean |du8| <= 0.6 % (refraction re-hit chaos:
     intersect_sphere keeps only the near root and refracted rays start on the surface).
 """
@@ -32,7 +33,7 @@ def test_oracle_matches_reference_golden(name):
     if name in scenes.GLASS_GOLDENS:
         assert mean_pct <= 0.6, (name, mean_pct, exact)
     else:
-        assert exact >= 0.999 and d.max() <= 6, (name, exact, d.max())
+        assert exact >= 0.9998 and d.max() <= 5, (name, exact, d.max())
 
 
 def test_orphan_golden_materials_is_unpinned():
