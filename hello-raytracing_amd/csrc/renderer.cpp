@@ -497,8 +497,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             r->ring_slots = 0;
             r->fold_bytes = (uint64_t)chunk * frame_floats * 4u;
         } else {
-            // frames per launch: at most 48 jobs per tile (the done bits of the tile's fold word)
-            chunk = std::max(1u, std::min(count, 48u * jf));
+            // frames per launch: at most FOLD_MAX_JOBS jobs per tile (the done bits of the tile's fold word)
+            chunk = std::max(1u, std::min(count, hrt_dev::FOLD_MAX_JOBS * jf));
             const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
             // a power-of-two number of job slots (jf x 64 px x 16 B each) in the budget, at most one per job of a
             // launch; a device short of memory gets a halved budget instead of a failed draw

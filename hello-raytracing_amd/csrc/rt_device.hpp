@@ -81,6 +81,9 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 // fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue overruns
 constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
 
+// fold ring: jobs per tile and launch (the done bits of a tile's fold word, rt_kernels.hip)
+constexpr uint32_t FOLD_MAX_JOBS = 48;
+
 constexpr uint32_t LNODE_CAP = 192;
 constexpr uint32_t LNODE_DEPTH = 8;
 

@@ -102,7 +102,9 @@ __device__ __forceinline__ float exact_sphere_t(const KParams& P, const Ray& r, 
 // the pair index to this lane's list in LDS (ascending). Pass 2 resolves the few candidates with the
 // reference's exact arithmetic in slot order, so `t > 0 && t < best` and first-slot-wins ties are
 // reproduced literally. A lane whose list overflows falls back to the full exact scan.
-constexpr int CAND_CAP = 15;  // list entries per lane; slot CAND_CAP is a write sink past overflow
+// list entries per lane; slot CAND_CAP is a write sink past overflow (14, not 15: the wave job words then fit
+// beside the mixed deferred-scan kernels' 32 KB of LDS at 5 workgroups per CU)
+constexpr int CAND_CAP = 14;
 
 __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray& r, float& best,
                                                      uint16_t* __restrict__ lds_list) {
@@ -918,8 +920,9 @@ __device__ __forceinline__ uint32_t ring_off(uint32_t slot, uint32_t fj, uint32_
 
 // Per-tile fold word (64 bits): bit c = job c has all its samples stored (c < 48), bits 48-54 = jobs folded
 // (the cursor), bit 63 = fold lock.
-constexpr unsigned long long TF_LOCK = 1ull << 63, TF_DONE = (1ull << 48) - 1ull;
-constexpr uint32_t TF_CURSOR_SHIFT = 48, TF_MAX_JOBS = 48;
+constexpr unsigned long long TF_LOCK = 1ull << 63;
+constexpr uint32_t TF_CURSOR_SHIFT = 48;  // (jobs per tile and launch <= FOLD_MAX_JOBS, rt_device.hpp)
+static_assert(FOLD_MAX_JOBS <= TF_CURSOR_SHIFT, "done bits below the cursor");
 
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
     return ((unsigned long long)uniform(__shfl((uint32_t)(v >> 32), 0)) << 32) | uniform(__shfl((uint32_t)v, 0));
