@@ -478,11 +478,15 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         while ((2u << P.jf_log2) <= std::min(jf, 1024u)) P.jf_log2++;
         jf = 1u << P.jf_log2;
         // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a launch, then
-        // k_accumulate) when the budget holds at least min(count, 64) frames of colours, in launches of as many
-        // frames as it holds; else the fold ring in the budget (bounded memory, about 10 % slower: DESIGN.md §5).
+        // k_accumulate) when the budget holds at least min(count, 320) frames of colours, in launches of as many
+        // frames as it holds; else the fold ring in the budget (bounded memory: DESIGN.md §4). Shorter buffer
+        // launches lose to the ring (fewer jobs per tile spread the waves over more of the image: C3 at 82 /
+        // 164 / 344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1, the 1 GiB ring 30.2 / 8.1).
         size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
         const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
-        P.ring_mode = budget / (frame_floats * 4u) < std::min<uint32_t>(std::max(count, 1u), 64u) ? 1u : 0u;
+        P.ring_mode = budget / (frame_floats * 4u) < std::min<uint32_t>(std::max(count, 1u), 320u) ? 1u : 0u;
+        // measurements: HRT_FOLD_RING=0/1 forces the fold
+        if (const char* fr = std::getenv("HRT_FOLD_RING")) P.ring_mode = std::atoi(fr) ? 1u : 0u;
         uint32_t chunk = 1, log2s = 0;
         size_t zero_words = 0;
         if (!P.ring_mode) {

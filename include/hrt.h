@@ -69,8 +69,8 @@ typedef struct rt_params {
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; 32768. The sample buffer when it holds
-                                  min(frames, 64) frames of colours (launches of as many frames as it holds),
-                                  else the fold ring in this budget (bounded memory, slower)             */
+                                  min(frames, 320) frames of colours (launches of as many frames as it
+                                  holds), else the fold ring in this budget (bounded memory, slower)     */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
                                   power of two (at most 1024); default 0 = per kernel: 32 with the
                                   suspendable walks, 16 for the linear sphere scans                      */

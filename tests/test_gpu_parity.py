@@ -161,7 +161,7 @@ def test_auto_schedule_by_draw_size():
 
 def test_sample_queue_chunks_and_tris_mode():
     """Budgets too small for the sample buffer: fold rings smaller than the draw's jobs (1 and 2 MiB at 320x240:
-    32 and 64 job slots of 32 frames for 1200 jobs, so most jobs wait for their slot); a budget holding 64+
+    32 and 64 job slots of 32 frames for 1200 jobs, so most jobs wait for their slot); a budget holding 320+
     frames: the sample buffer in launches of that many frames; and the triangle program under the queue
     schedule."""
     sd = scenes.golden_scene("metal_materials", 320, 240)
@@ -177,15 +177,18 @@ def test_sample_queue_chunks_and_tris_mode():
         assert st.fold_ring == 1 and st.launches == 1, (st.fold_ring, st.launches)
         assert (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), st.fold_bytes
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
-    # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 64 MiB hold 72 frames -> launches of 72, 72, 56
+    # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 320 MiB hold 364 frames (>= 320: the sample buffer)
+    # -> 700 frames in launches of 364 and 336
+    per_frame = 1200 * 64 * 12
+    chunk = (320 << 20) // per_frame
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
-    ref.draw_frames(200, 1000, 10)
+    ref.draw_frames(700, 1000, 10)
     r = scenes.make_renderer(sd)
-    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=64)
-    r.draw_frames(200, 1000, 10)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=320)
+    r.draw_frames(700, 1000, 10)
     st = r.stats()
-    assert st.fold_ring == 0 and st.launches == 6 and st.fold_bytes == 72 * 1200 * 64 * 12, (st.launches, st.fold_bytes)
+    assert st.fold_ring == 0 and st.launches == 4 and st.fold_bytes == chunk * per_frame, (st.launches, st.fold_bytes)
     np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     scene = hrt.SceneTris.new_suzane(96, 72)
     scene.init()
