@@ -485,21 +485,15 @@ __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, in
     h.front = front;
 }
 
-#ifndef HRT_HEAP_PAIR
-#define HRT_HEAP_PAIR 1  // heap_run: sibling-pair node loads (see heap_run)
-#endif
-
 // intersect_node (shader_tris.wgsl:150-159); inv = 1/d is the same value for every node of a query.
-__device__ __forceinline__ bool box_hit(const float4& mn, const float4& mx, const f3& o, const f3& inv) {
+__device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3& o, const f3& inv) {
+    const float4 mn = P.nodes[2 * i];
+    const float4 mx = P.nodes[2 * i + 1];
     const float t0x = (mn.x - o.x) * inv.x, t0y = (mn.y - o.y) * inv.y, t0z = (mn.z - o.z) * inv.z;
     const float t1x = (mx.x - o.x) * inv.x, t1y = (mx.y - o.y) * inv.y, t1z = (mx.z - o.z) * inv.z;
     const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmin_ieee(t0z, t1z));
     const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmax_ieee(t0z, t1z));
     return tmin <= tmax && tmax >= 0.0f;
-}
-
-__device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3& o, const f3& inv) {
-    return box_hit(P.nodes[2 * i], P.nodes[2 * i + 1], o, inv);
 }
 
 // intersect_triangle, Moller-Trumbore (shader_tris.wgsl:161-202): the candidate t, or -1 when the
@@ -597,7 +591,6 @@ struct HeapWalk {
     uint32_t i, step;
     float best;       // starts at the sphere winner's t (triangles must beat it: `t >= best` rejects)
     int bj;           // winning triangle (-1: none)
-    uint32_t sib;     // HRT_HEAP_PAIR: bit d = intersect_node of the right sibling at depth d, tested with its left
 };
 
 __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W) {
@@ -606,10 +599,9 @@ __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W
     W.step = 0u;
     W.best = best;
     W.bj = -1;
-    W.sib = 0u;
 }
 
-template <bool SUSPEND, bool PAIR = false>
+template <bool SUSPEND>
 __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand,
                                          uint32_t below) {
     const f3 inv = W.inv;
@@ -618,105 +610,37 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
     uint32_t walking = 1u;  // an integer, not an i1 lane mask (see bvh_run)
     float best = W.best;
     int bj = W.bj;
-    if constexpr (PAIR) {
-        // Sibling pairs: the walk reaches an even node only by descending, and the odd node after it (its right
-        // sibling) only after the even one's subtree, so one 64 B load of the pair (2k, 2k+1) runs both
-        // intersect_node tests when the even node is visited; the right one's result waits in a bit per depth.
-        // Per wave round a lane then visits odd nodes and leaves with no load until it reaches an even node (or
-        // the root), whose pair load is the round's only memory step. Same visits in the same order, same
-        // node/triangle counts and step cap, same triangle order: the reference walk exactly.
-        uint32_t sib = W.sib;
-        while (true) {
-            while (walking != 0u && __ballot(nc == TRI_BATCH) == 0ull) {
-                bool need = false;
-                while (walking != 0u && nc < TRI_BATCH) {
-                    bool advance = true;
-                    if (i < n) {
-                        if ((i & 1u) == 0u || i == 1u) {
-                            need = true;
-                            break;
-                        }
-                        tally.nodes++;
-                        if ((sib >> (31u - __builtin_clz(i))) & 1u) {
-                            i *= 2u;
-                            advance = false;
-                        }
-                    } else {
-                        const uint32_t j = i - n;
-                        if (j >= m) {
-                            walking = 0u;
-                            advance = false;
-                        } else {
-                            tally.tris++;
-                            cand[(nc++) * 256u] = j;
-                        }
-                    }
-                    if (advance) {
-                        i >>= __builtin_ctz(~i);
-                        if (i == 0u) walking = 0u;
-                        i++;
-                    }
-                    if (++step == 600u) walking = 0u;
+    while (true) {
+        while (walking != 0u && __ballot(nc == TRI_BATCH) == 0ull) {
+            bool advance = true;
+            if (i < n) {
+                tally.nodes++;
+                if (node_hit(P, i, r.o, inv)) {
+                    i *= 2u;
+                    advance = false;
                 }
-                if (need) {
-                    const uint32_t b = i & ~1u;
-                    const uint32_t rb = b + 1u < n ? b + 1u : b;  // a right sibling past n is a leaf: bit unused
-                    const bool hl = box_hit(P.nodes[2u * b], P.nodes[2u * b + 1u], r.o, inv);
-                    const bool hr = box_hit(P.nodes[2u * rb], P.nodes[2u * rb + 1u], r.o, inv);
-                    const uint32_t d = 31u - __builtin_clz(i);
-                    sib = (sib & ~(1u << d)) | ((uint32_t)hr << d);
-                    tally.nodes++;
-                    if ((i & 1u) ? hr : hl) {
-                        i *= 2u;
-                    } else {
-                        i >>= __builtin_ctz(~i);
-                        if (i == 0u) walking = 0u;
-                        i++;
-                    }
-                    if (++step == 600u) walking = 0u;
-                }
-            }
-            for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
-            nc = 0u;
-            if (walking == 0u) break;
-            if constexpr (SUSPEND) {
-                if ((uint32_t)__popcll(__ballot(1)) < below) break;
-            }
-        }
-        W.sib = sib;
-    } else {
-        while (true) {
-            while (walking != 0u && __ballot(nc == TRI_BATCH) == 0ull) {
-                bool advance = true;
-                if (i < n) {
-                    tally.nodes++;
-                    if (node_hit(P, i, r.o, inv)) {
-                        i *= 2u;
-                        advance = false;
-                    }
+            } else {
+                const uint32_t j = i - n;
+                if (j >= m) {
+                    walking = 0u;
+                    advance = false;
                 } else {
-                    const uint32_t j = i - n;
-                    if (j >= m) {
-                        walking = 0u;
-                        advance = false;
-                    } else {
-                        tally.tris++;
-                        cand[(nc++) * 256u] = j;
-                    }
+                    tally.tris++;
+                    cand[(nc++) * 256u] = j;
                 }
-                if (advance) {
-                    i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
-                    if (i == 0u) walking = 0u;
-                    i++;
-                }
-                if (++step == 600u) walking = 0u;  // the reference's step cap
             }
-            for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
-            nc = 0u;
-            if (walking == 0u) break;
-            if constexpr (SUSPEND) {
-                if ((uint32_t)__popcll(__ballot(1)) < below) break;
+            if (advance) {
+                i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
+                if (i == 0u) walking = 0u;
+                i++;
             }
+            if (++step == 600u) walking = 0u;  // the reference's step cap
+        }
+        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
+        nc = 0u;
+        if (walking == 0u) break;
+        if constexpr (SUSPEND) {
+            if ((uint32_t)__popcll(__ballot(1)) < below) break;
         }
     }
     W.i = i;
@@ -2074,7 +1998,7 @@ k_trace_split_tris(const KParams P) {
             }
         }
         if (have && qs == 3u) {
-            if (heap_run<true, HRT_HEAP_PAIR && SCAN != SCAN_BVH>(P, ray, W, tally, cand, suspend_below)) qs = 4u;
+            if (heap_run<true>(P, ray, W, tally, cand, suspend_below)) qs = 4u;
         }
         if (have && qs >= 4u) {
             bool done = true;
