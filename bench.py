@@ -6,10 +6,15 @@ mode. One STEP = one full render of that image (all 1024 frames, all rows) into 
 buffer, scene already resident in HBM. A "ray" is one closest-hit query (primary + every scattered ray,
 terminating miss included), counted exactly by the kernel.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the image is split by
-interleaved rows (rank r renders rows r, r+N, ...: sky-heavy top rows spread evenly), every rank renders
-its rows for all frames, then one RCCL gather over xGMI assembles the full image on rank 0 (inside the
-timed region). Total work is fixed as N grows -> "scaling": "strong"; `value` is the whole-job rate.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the image is split into
+8-row blocks dealt round-robin (rank r renders rows 8r..8r+7, 8(r+N)..8(r+N)+7, ...: whole 8x8 tile rows, so
+the sample queue's tiles stay compact, and the sky-heavy top rows spread evenly), every rank renders its rows
+for all frames, then one RCCL gather over xGMI assembles the full image on rank 0 (inside the timed region).
+Total work is fixed as N grows -> "scaling": "strong"; `value` is the whole-job rate.
+
+Single-GPU proxy of that split (`--emulate-ranks N`, default 8 on a one-rank run): after the timed region,
+every rank's share is rendered on this GPU in turn with the same step; the predicted N-GPU step time is the
+slowest share's, and `emulated_split.efficiency` = full-image time / (N x slowest share).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), plus `roofline` (FP32-VALU bound; HIP-event
 time of the render kernel on the stream it runs on) and `cpu_baseline` (the CPU oracle on a bounded sample).
@@ -134,20 +139,22 @@ def launcher_selftest(args) -> int:
     import torch
     import torch.distributed as dist
 
-    from hrt.parallel import gather_image, rows_of
+    from hrt.parallel import gather_image, max_rows, rank_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
     H, W = 37, 5
-    n = rows_of(rank, world, H)
-    part = torch.zeros((-(-H // world), W, 3), dtype=torch.float32)
-    part[:n] = torch.arange(rank, H, world, dtype=torch.float32)[:, None, None]
-    full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0)
+    block = args.row_block
+    rows = rank_rows(rank, world, H, block)
+    part = torch.zeros((max_rows(world, H, block), W, 3), dtype=torch.float32)
+    part[: len(rows)] = torch.from_numpy(rows.astype("float32"))[:, None, None]
+    full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0, block=block)
     if rank == 0:
         ok = bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32)))
         print(json.dumps({"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}",
+                          "row_block": block,
                           "verify_gather_bitwise": ok}), flush=True)
     if world > 1:
         dist.barrier()
@@ -168,6 +175,7 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
     return {
         "value": round(q / dt / 1e6, 3),
         "unit": "Mrays/s",
+        "samples_per_s": round(n * sd.width * frames / dt, 1),
         "cores": threads,
         "kind": "port",
         "algorithm": (f"linear-scan oracle: every ray tests all {len(sd.spheres)} sphere slots (the reference's "
@@ -179,6 +187,66 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
 
 
 MODE_NAMES = {0: "sphere", 1: "tris", 2: "mixed"}
+
+
+def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_rays: float) -> dict:
+    """Single-GPU proxy of the n-rank row split: every rank's share (rank_params(k, n, row_block)) rendered on
+    this GPU in turn with the bench's step (reset, draw all frames, copy the image out, synchronise), warmed up
+    and timed like the full image. On n GPUs the step takes the slowest share (+ the gather of <= 3 MB per
+    rank for C3, ~0.1 ms over xGMI), so efficiency = full-image step / (n x slowest share). The shares are
+    also put back together and compared with the full image bit for bit."""
+    import numpy as np
+    import torch
+
+    import scenes
+    from hrt.parallel import assemble, rank_params
+
+    shares, parts = [], []
+    for k in range(n):
+        rk = scenes.make_renderer(sd)
+        rk.set_params(**rank_params(k, n, args.row_block), **knobs)
+        buf = torch.zeros((rk.local_rows, sd.width, 3), dtype=torch.float32, device="cuda")
+
+        def share_step():
+            rk.reset_frame_count()
+            rk.draw_frames(sd.frames, 1000, 10)
+            rk.copy_image_to_device(buf.data_ptr(), buf.numel())
+            return rk.stats()
+
+        for _ in range(max(1, args.warmup)):
+            share_step()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        rays = trace_ms = 0.0
+        for _ in range(args.steps):
+            st = share_step()
+            rays += st.queries
+            trace_ms += st.trace_ms
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / args.steps
+        shares.append({"rank": k, "rows": rk.local_rows, "ms_per_step": round(dt * 1e3, 3),
+                       "trace_ms": round(trace_ms / args.steps, 3), "mrays_s": round(rays / args.steps / dt / 1e6, 1)})
+        parts.append(buf.cpu())
+        rk.close()
+        del buf
+        log(f"emulated rank {k}/{n}: {shares[-1]}")
+    slowest = max(s["ms_per_step"] for s in shares)
+    same = None
+    if full_img is not None:
+        whole = assemble(parts, sd.height, n, block=args.row_block)
+        same = bool(torch.equal(whole.view(torch.int32), full_img.cpu().view(torch.int32)))
+    return {
+        "ranks": n,
+        "row_block": args.row_block,
+        "full_ms_per_step": round(full_s * 1e3, 3),
+        "full_mrays_s": round(full_rays / full_s / 1e6, 1),
+        "predicted_ms_per_step": slowest,
+        "predicted_mrays_s": round(full_rays / (slowest * 1e-3) / 1e6, 1),
+        "efficiency": round(full_s * 1e3 / (n * slowest), 4),
+        "rank0_mrays_s": shares[0]["mrays_s"],
+        "bitwise_equal_full_image": same,
+        "per_rank": shares,
+    }
 
 
 def main() -> int:
@@ -200,6 +268,8 @@ def main() -> int:
                          "(default: the library's)")
     ap.add_argument("--queue-budget-mb", type=int, default=None,
                     help="sample queue: colour-buffer budget per chunk in MiB (default: the library's)")
+    ap.add_argument("--fold", type=int, default=None,
+                    help="sample queue colour fold: 0 auto, 1 sample buffer + k_accumulate, 2 fold ring")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -211,6 +281,12 @@ def main() -> int:
     ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=128)
+    ap.add_argument("--row-block", type=int, default=8,
+                    help="multi-GPU split: rows per block dealt round-robin (8 = whole 8x8 tile rows; 1 = single "
+                         "interleaved rows)")
+    ap.add_argument("--emulate-ranks", type=int, default=None,
+                    help="single-GPU proxy of the N-rank split: render every rank's share here in turn after the "
+                         "timed region (default 8 on a one-rank run, 0 = off)")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU-only rehearsal of the multi-rank path (self-launch, gloo, row-tile gather): no GPU")
     args = ap.parse_args()
@@ -229,7 +305,7 @@ def main() -> int:
 
     import hrt  # noqa: F401  (loads lib/libhrt.so)
     import scenes
-    from hrt.parallel import gather_image
+    from hrt.parallel import gather_image, max_rows, rank_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -263,11 +339,13 @@ def main() -> int:
         extra["job_frames"] = args.job_frames
     if args.queue_budget_mb is not None:
         extra["queue_budget_mb"] = args.queue_budget_mb
-    r.set_params(row0=rank, row_step=world, frames_per_launch=args.frames_per_launch, variant=args.variant,
-                 schedule=args.schedule, tri_bvh=args.tri_bvh, **extra)
+    if args.fold is not None:
+        extra["fold"] = args.fold
+    knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
+                 tri_bvh=args.tri_bvh, **extra)
+    r.set_params(**rank_params(rank, world, args.row_block), **knobs)
     local_rows = r.local_rows
-    max_rows = (sd.height + world - 1) // world
-    part = torch.zeros((max_rows, sd.width, 3), dtype=torch.float32, device=dev)
+    part = torch.zeros((max_rows(world, sd.height, args.row_block), sd.width, 3), dtype=torch.float32, device=dev)
     gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
     full = torch.empty((sd.height, sd.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
 
@@ -281,7 +359,7 @@ def main() -> int:
         r.draw_frames(sd.frames, 1000, 10)
         r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
         st = r.stats()
-        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full)
+        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=args.row_block)
         if world > 1:
             # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
             # renderer's own stream, which does not order against it: finish the gather first
@@ -330,6 +408,10 @@ def main() -> int:
             f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
     barrier()
     elapsed = time.perf_counter() - t0
+    emulated = None
+    n_emul = args.emulate_ranks if args.emulate_ranks is not None else (8 if world == 1 else 0)
+    if world == 1 and n_emul > 1:
+        emulated = emulate_split(sd, knobs, n_emul, args, full, elapsed / args.steps, queries / args.steps)
 
     stats_t = torch.tensor([elapsed, float(queries), trace_ms, float(trace_launches), float(box_tests),
                             float(sphere_tests), float(node_tests), float(tri_tests), kernel_ms],
@@ -383,6 +465,8 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 2),
+            # SURVEY 8(d) / BASELINE.md 3: pixel-samples per second (W x H x spp per step)
+            "samples_per_s": round(sd.width * sd.height * sd.frames * args.steps / t_max, 1),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -399,6 +483,7 @@ def main() -> int:
                 "rays_per_step": round(total_q / args.steps),
                 "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
                 "parallelism": f"rows{world}",
+                "row_block": args.row_block,
                 # how the sample queue folded the colours in frame order (rt_params.queue_budget_mb):
                 # "sample-buffer" (+ k_accumulate) or the bounded-memory "fold-ring"; device bytes it used
                 "fold": ("fold-ring" if st_last.fold_ring else "sample-buffer") if schedule == 2 else "in-register",
@@ -441,6 +526,8 @@ def main() -> int:
                 "pmc": pmc_view(pmc),
             },
         }
+        if emulated is not None:
+            out["emulated_split"] = emulated
         if not args.no_cpu_baseline and world == 1:
             log("cpu baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline(sd, cpu_threads(), args.cpu_rows, args.cpu_frames)
@@ -451,8 +538,7 @@ def main() -> int:
         if args.verify:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)
-            ref_r.set_params(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
-                             tri_bvh=args.tri_bvh, **extra)
+            ref_r.set_params(**knobs)
             ref_r.draw_frames(sd.frames, 1000, 10)
             ref_img = torch.from_numpy(ref_r.read_image())
             same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))

@@ -5,7 +5,9 @@
 // The parser also reproduces tobj's per-model vertex numbering (default LoadOptions: single_index =
 // false, triangulate = false -> positions are de-duplicated per model by position index, in order of
 // first reference), so Mesh::vertices.len() matches the reference's unit tests (mesh.rs:64-89).
-// Like the reference, any tobj LoadError (bad float, out-of-bounds face index) yields an EMPTY mesh.
+// Like the reference, any tobj LoadError (bad float, out-of-bounds face index, a line that is not UTF-8:
+// BufRead::lines() -> ReadError) yields an EMPTY mesh. Words are split as Rust's str::split_whitespace does
+// (Unicode White_Space, not only ASCII).
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
@@ -36,8 +38,8 @@ struct Parser {
         errno = 0;
         float v = std::strtof(s, &end);
         if (end != s + w.size()) return false;
-        // Rust's f32::from_str rejects hex floats; strtof accepts them.
-        if (w.find('x') != std::string::npos || w.find('X') != std::string::npos) return false;
+        // Rust's f32::from_str rejects hex floats and "nan(...)"; strtof accepts them.
+        if (w.find_first_of("xX(") != std::string::npos) return false;
         *out = v;
         return true;
     }
@@ -63,7 +65,7 @@ struct Parser {
                     m.indices.push_back(it->second);
                     continue;
                 }
-                if (v < 0 || (size_t)v * 3 + 2 >= pos.size()) { failed = true; return; }  // FaceVertexOutOfBounds
+                if (v < 0 || (size_t)v >= pos.size() / 3) { failed = true; return; }  // FaceVertexOutOfBounds
                 uint32_t next = (uint32_t)index_map.size();
                 m.positions.push_back(pos[(size_t)v * 3]);
                 m.positions.push_back(pos[(size_t)v * 3 + 1]);
@@ -76,15 +78,47 @@ struct Parser {
         faces.clear();
     }
 
+    // One UTF-8 scalar value at ln[i]: its length in bytes (0 = invalid: overlong, surrogate, > U+10FFFF,
+    // truncated) and the code point.
+    static size_t utf8_at(const std::string& ln, size_t i, uint32_t* cp) {
+        const unsigned char c = (unsigned char)ln[i];
+        if (c < 0x80) { *cp = c; return 1; }
+        size_t n = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC2 ? 2 : 0;
+        if (n == 0 || c > 0xF4 || i + n > ln.size()) return 0;
+        uint32_t v = c & (0x7Fu >> n);
+        for (size_t k = 1; k < n; k++) {
+            const unsigned char d = (unsigned char)ln[i + k];
+            if ((d & 0xC0) != 0x80) return 0;
+            v = (v << 6) | (d & 0x3Fu);
+        }
+        if ((n == 3 && v < 0x800) || (n == 4 && (v < 0x10000 || v > 0x10FFFF)) || (v >= 0xD800 && v <= 0xDFFF)) return 0;
+        *cp = v;
+        return n;
+    }
+    // char::is_whitespace (Unicode White_Space)
+    static bool is_ws(uint32_t c) {
+        return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+               (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+    }
+
     void line(const std::string& ln) {
         std::vector<std::string> w;
-        size_t i = 0;
+        size_t i = 0, s = 0;
+        bool in_word = false;
         while (i < ln.size()) {
-            while (i < ln.size() && std::isspace((unsigned char)ln[i])) i++;
-            size_t s = i;
-            while (i < ln.size() && !std::isspace((unsigned char)ln[i])) i++;
-            if (i > s) w.push_back(ln.substr(s, i - s));
+            uint32_t cp = 0;
+            const size_t n = utf8_at(ln, i, &cp);
+            if (n == 0) { failed = true; return; }  // not UTF-8: tobj's lines() fails with ReadError
+            if (is_ws(cp)) {
+                if (in_word) w.push_back(ln.substr(s, i - s));
+                in_word = false;
+            } else if (!in_word) {
+                in_word = true;
+                s = i;
+            }
+            i += n;
         }
+        if (in_word) w.push_back(ln.substr(s));
         if (w.empty()) return;
         const std::string& key = w[0];
         if (key == "v") {

@@ -140,7 +140,7 @@ void Tree::build(unsigned threads) {
     const size_t n = next_power_of_two(m);
     std::vector<uint32_t> perm(m);
     for (size_t k = 0; k < m; k++) perm[k] = (uint32_t)k;
-    const float* key = &triangles.data()->custom.x;  // custom of triangle k at key[k * 16 + axis]
+    const float* key = m ? &triangles[0].custom.x : nullptr;  // custom of triangle k at key[k * 16 + axis]
     static_assert(sizeof(Triangle) == 64, "Triangle stride");
     // sort (key, index) pairs in a per-thread buffer: contiguous keys instead of one gather per compare
     using Pairs = std::vector<std::pair<float, uint32_t>>;

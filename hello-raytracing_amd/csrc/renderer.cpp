@@ -25,6 +25,7 @@ hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, h
 hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 const char* hrt_last_kernel();
+void hrt_reset_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
 
 namespace {
@@ -51,6 +52,7 @@ struct DevBuf {
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
+    uint64_t bytes() const { return ptr ? (uint64_t)cap * sizeof(T) : 0u; }
     void release() {
         if (ptr) (void)hipFree(ptr);
         ptr = nullptr;
@@ -58,15 +60,15 @@ struct DevBuf {
     }
 };
 
+// fail_above: fault injection for tests (rt_params.fail_alloc_above_mb), an allocation above that many bytes
+// fails as a refused hipMalloc would (0 = off)
 template <typename T>
-int ensure(DevBuf<T>& b, size_t n) {
+int ensure(DevBuf<T>& b, size_t n, size_t fail_above = 0) {
     if (n <= b.cap && b.ptr) return RT_OK;
     b.release();
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-    // fault injection for tests: HRT_FAIL_ALLOC_ABOVE_MB=m makes every device allocation above m MiB fail
-    static const char* cap_env = std::getenv("HRT_FAIL_ALLOC_ABOVE_MB");
-    if (cap_env && bytes > ((size_t)std::strtoull(cap_env, nullptr, 10) << 20))
-        return fail(RT_ERR_ALLOC, "hipMalloc: injected failure (HRT_FAIL_ALLOC_ABOVE_MB)");
+    if (fail_above && bytes > fail_above)
+        return fail(RT_ERR_ALLOC, "hipMalloc: injected failure (rt_params.fail_alloc_above_mb)");
     hipError_t e = hipMalloc((void**)&b.ptr, bytes);
     if (e != hipSuccess) {
         b.ptr = nullptr;
@@ -75,6 +77,39 @@ int ensure(DevBuf<T>& b, size_t n) {
     b.cap = std::max<size_t>(n, 1);
     return RT_OK;
 }
+
+// ensure() for the sample queue's colour-fold memory, which must stay within rt_params.queue_budget_mb: a buffer
+// left larger by an earlier draw is given back when it exceeds `budget` bytes or twice what this draw needs.
+template <typename T>
+int ensure_within(DevBuf<T>& b, size_t n, size_t budget, size_t fail_above) {
+    if (b.ptr && (b.cap * sizeof(T) > budget || b.cap > 2 * std::max<size_t>(n, 1))) b.release();
+    return ensure(b, n, fail_above);
+}
+
+// Makes `device` current for one rt_* call and restores the caller's device after it: a renderer's memory, stream
+// and launches stay on the GPU it was created on whatever device the calling thread has current (one process
+// driving several GPUs, or a caller that switches devices between calls).
+struct DeviceScope {
+    int prev = -1, rc = RT_OK;
+    explicit DeviceScope(int device) {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) {
+            rc = fail(RT_ERR_DEVICE, "hipGetDevice failed");
+            return;
+        }
+        if (cur == device) return;
+        if (hipSetDevice(device) != hipSuccess) {
+            rc = fail(RT_ERR_DEVICE, "hipSetDevice to the renderer's device failed");
+            return;
+        }
+        prev = cur;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
 
 int check_device(int* dev_out) {
     int n = 0;
@@ -90,9 +125,15 @@ int check_device(int* dev_out) {
     return RT_OK;
 }
 
-uint32_t local_rows_of(uint32_t H, uint32_t row0, uint32_t step) {
+// Rows owned by a renderer: blocks of `block` rows starting at row0, row0 + step*block, ... (block 1: the
+// interleaved rows row0, row0 + step, ...); the last block may be cut by the image bottom.
+uint32_t local_rows_of(uint32_t H, uint32_t row0, uint32_t step, uint32_t block) {
     if (row0 >= H || step == 0) return 0;
-    return (H - row0 + step - 1) / step;
+    block = std::max(block, 1u);
+    const uint64_t stride = (uint64_t)step * block;
+    const uint64_t nblocks = ((uint64_t)H - row0 + stride - 1) / stride;
+    const uint64_t last0 = row0 + (nblocks - 1) * stride;  // first row of the last block
+    return (uint32_t)((nblocks - 1) * block + std::min<uint64_t>(block, H - last0));
 }
 
 }  // namespace
@@ -152,7 +193,14 @@ struct rt_renderer {
     uint64_t fold_bytes = 0;  // device memory of the last sample-queue draw's colour fold (rt_stats.fold_bytes)
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
-    uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step); }
+    uint32_t row_block() const { return std::max(params.row_block, 1u); }
+    uint64_t device_bytes() const {
+        return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
+               bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
+               wave_trace.bytes();
+    }
+    uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
 };
 
@@ -406,6 +454,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.m = r->mode == RT_MODE_SPHERE ? 0u : r->bvh_m;
     P.row0 = r->params.row0;
     P.row_step = r->params.row_step;
+    P.row_block = r->row_block();
+    P.row_stride = r->params.row_step * P.row_block;
     P.nrows = r->local_rows();
     P.image = r->image.ptr;
     P.sph_geo = r->sph_geo.ptr;
@@ -463,6 +513,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->last_suspend = 0;
 
     uint32_t launches = 0;
+    hrt_reset_last_kernel();  // (a draw that launches nothing reports no kernel)
     if (schedule == RT_SCHEDULE_QUEUE) {
         r->trace_pairs_pending = 0;
         P.tiles_w = (r->width + 7u) / 8u;
@@ -485,14 +536,19 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
         const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
         P.ring_mode = budget / (frame_floats * 4u) < std::min<uint32_t>(std::max(count, 1u), 320u) ? 1u : 0u;
-        // measurements: HRT_FOLD_RING=0/1 forces the fold
-        if (const char* fr = std::getenv("HRT_FOLD_RING")) P.ring_mode = std::atoi(fr) ? 1u : 0u;
+        if (r->params.fold == RT_FOLD_BUFFER) P.ring_mode = 0u;  // forced (measurements, tests)
+        if (r->params.fold == RT_FOLD_RING) P.ring_mode = 1u;
+        const size_t fail_above = (size_t)r->params.fail_alloc_above_mb << 20;
         uint32_t chunk = 1, log2s = 0;
         size_t zero_words = 0;
         if (!P.ring_mode) {
+            r->ring.release();  // the other fold's memory: the draw's colour memory stays within the budget
+            r->ring_ctl.release();
             chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
             // a device short of memory gets smaller launches, down to one frame, instead of a failed draw
-            while (count && (rc = ensure(r->samples, (size_t)chunk * frame_floats)) == RT_ERR_ALLOC && chunk > 1u) {
+            const size_t buf_budget = std::max(budget, frame_floats * 4u);
+            while ((rc = ensure_within(r->samples, (size_t)chunk * frame_floats, buf_budget, fail_above)) == RT_ERR_ALLOC &&
+                   chunk > 1u) {
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
                 chunk = (chunk + 1u) / 2u;
             }
@@ -501,35 +557,32 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             r->ring_slots = 0;
             r->fold_bytes = (uint64_t)chunk * frame_floats * 4u;
         } else {
+            r->samples.release();
             // frames per launch: at most FOLD_MAX_JOBS jobs per tile (the done bits of the tile's fold word)
             chunk = std::max(1u, std::min(count, hrt_dev::FOLD_MAX_JOBS * jf));
             const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
             // a power-of-two number of job slots (jf x 64 px x 16 B each) in the budget, at most one per job of a
             // launch; a device short of memory gets a halved budget instead of a failed draw
             budget = std::min<size_t>(budget, 2047ull << 20);
-            auto plan = [&]() {
+            const uint64_t jobs = (uint64_t)ntiles * nchunks_max;
+            for (;;) {
                 const size_t fit = std::max<size_t>(1, budget / ((size_t)jf << 10));
-                const uint64_t jobs = (uint64_t)ntiles * nchunks_max;
                 log2s = 0;
                 while ((2ull << log2s) <= fit && (1ull << log2s) < jobs && log2s < 20u) log2s++;
-                // tests: HRT_RING_SLOTS_MAX=n caps the slots (n a power of two), so jobs wait for their slot
-                static const char* cap_env = std::getenv("HRT_RING_SLOTS_MAX");
-                if (cap_env)
-                    while (log2s > 0 && (1ull << log2s) > std::strtoull(cap_env, nullptr, 10)) log2s--;
-            };
-            plan();
-            zero_words = 2ull * ntiles + (4ull << log2s) + 4u;  // (log2s only shrinks below)
-            if (count) {
-                for (;;) {
-                    rc = ensure(r->ring, ((size_t)jf << log2s) * 64u);
-                    if (!rc) rc = ensure(r->ring_ctl, zero_words + (size_t)ntiles * nchunks_max);
-                    if (rc != RT_ERR_ALLOC || budget <= ((size_t)jf << 10)) break;
-                    (void)hipGetLastError();
-                    budget /= 2u;
-                    plan();
-                }
-                if (rc) return rc;
+                // rt_params.ring_slots_max caps the slots (tests: jobs then wait in the free queue for a slot)
+                while (r->params.ring_slots_max && log2s > 0 && (1ull << log2s) > r->params.ring_slots_max) log2s--;
+                zero_words = 2ull * ntiles + (4ull << log2s) + 4u;
+                const size_t ring_floats4 = ((size_t)jf << log2s) * 64u;
+                rc = ensure_within(r->ring, ring_floats4, std::max(budget, ring_floats4 * 16u), fail_above);
+                const size_t ctl_words = zero_words + (size_t)ntiles * nchunks_max;
+                if (!rc) rc = ensure_within(r->ring_ctl, ctl_words, ctl_words * 4u, fail_above);
+                if (rc != RT_ERR_ALLOC || budget <= ((size_t)jf << 10)) break;
+                (void)hipGetLastError();
+                r->ring.release();  // retry both with half the budget
+                r->ring_ctl.release();
+                budget /= 2u;
             }
+            if (rc) return rc;
             P.ring = r->ring.ptr;
             P.ring_log2 = log2s;
             P.ring_bytes = (uint32_t)(((size_t)jf << log2s) * 1024u);
@@ -594,6 +647,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         r->stats.fold_ring = P.ring_mode;
         r->stats.fold_bytes = r->fold_bytes;
     }
+    r->stats.device_bytes = r->device_bytes();
     r->timing_pending = true;
     return RT_OK;
 }
@@ -608,8 +662,9 @@ int finish_stats(rt_renderer* r) {
     HIP_TRY(hipMemcpy(q, r->counter.ptr, RT_RAW_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(wd, r->counter.ptr + hrt_dev::WATCHDOG, sizeof wd, hipMemcpyDeviceToHost));
     if (wd[0] || wd[3]) {  // waves gave up waiting for a fold-ring slot: the image is incomplete; report, do not hang
-        // diagnostics: HRT_RING_DUMP=path writes the fold-ring control words (tile done masks, tile locks and
+        // diagnostic build: HRT_RING_DUMP=path writes the fold-ring control words (tile done masks, tile locks and
         // cursors, free queue, tail) and the counters as raw little-endian words
+#ifdef HRT_STAMPS
         if (const char* path = std::getenv("HRT_RING_DUMP")) {
             std::vector<uint32_t> ctl(r->ring_ctl_words);
             if (!ctl.empty())
@@ -624,6 +679,7 @@ int finish_stats(rt_renderer* r) {
                 std::fclose(f);
             }
         }
+#endif
         char msg[200];
         std::snprintf(msg, sizeof msg, "sample queue: %llu waves waited > 2^24 idle rounds for a fold-ring slot "
                       "(last: job %llu, entry flags %llx); %llu free-queue overruns", wd[0], wd[1], wd[2], wd[3]);
@@ -653,6 +709,28 @@ int finish_stats(rt_renderer* r) {
     r->stats.suspend_below = r->last_suspend;
     r->timing_pending = false;
     return RT_OK;
+}
+
+void delete_buffers(rt_renderer* r) {
+    r->image.release();
+    r->sph_geo.release();
+    r->sph_aux.release();
+    r->sph_pairs.release();
+    r->bvh_nodes.release();
+    r->bvh_sph.release();
+    r->bvh_hnodes.release();
+    r->bvh_slot.release();
+    r->bvh_large.release();
+    r->nodes.release();
+    r->tris.release();
+    r->mats.release();
+    r->tb_hnodes.release();
+    r->tb_order.release();
+    r->counter.release();
+    r->samples.release();
+    r->ring.release();
+    r->ring_ctl.release();
+    r->wave_trace.release();
 }
 
 }  // namespace
@@ -690,6 +768,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.min_sphere_slots = mode == RT_MODE_SPHERE ? RT_MAX_OBJECT_IN_SCENE : 0u;
     r->params.row0 = 0;
     r->params.row_step = 1;
+    r->params.row_block = 1;
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
     // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one chunk (one k_trace launch per draw, one launch
@@ -718,15 +797,9 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
 
 int rt_destroy(rt_renderer* r) {
     if (!r) return RT_OK;
+    DeviceScope ds(r->device);  // (frees on the renderer's device even if switching failed)
     if (r->stream) (void)hipStreamSynchronize(r->stream);
-    r->image.release();
-    r->sph_geo.release();
-    r->sph_aux.release();
-    r->sph_pairs.release();
-    r->nodes.release();
-    r->tris.release();
-    r->mats.release();
-    r->counter.release();
+    delete_buffers(r);
     for (hipEvent_t e : r->ev_trace) (void)hipEventDestroy(e);
     if (r->ev_start) (void)hipEventDestroy(r->ev_start);
     if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
@@ -743,13 +816,19 @@ int rt_get_params(const rt_renderer* r, rt_params* out) {
 
 int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
+    if ((uint64_t)p->row_step * std::max(p->row_block, 1u) > (1ull << 30))
+        return fail(RT_ERR_ARG, "rt_set_params: row_step x row_block too large");
     if (p->variant != 0 && p->variant != 1 && p->variant != 3 && p->variant != 4)
         return fail(RT_ERR_ARG, "rt_set_params: unknown variant (0 auto, 1 simple, 3 deferred, 4 culling BVH)");
     if (p->schedule > RT_SCHEDULE_QUEUE) return fail(RT_ERR_ARG, "rt_set_params: unknown schedule");
     if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     if (p->suspend_below > 64) return fail(RT_ERR_ARG, "rt_set_params: suspend_below must be 0..64");
-    const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step;
+    if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
+    const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
+                              std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;
     if (rows_changed) {
@@ -770,6 +849,8 @@ int rt_set_camera(rt_renderer* r, const void* camera80) {
 
 int rt_set_spheres(rt_renderer* r, const void* spheres48, uint32_t n) {
     if (!r || (n && !spheres48)) return fail(RT_ERR_ARG, "rt_set_spheres: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     // a hit carries its slot in 29 bits (rt_kernels.hip Hit::id)
     if (n >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_spheres: more than 2^28 spheres");
     r->spheres.resize(n);
@@ -780,6 +861,8 @@ int rt_set_spheres(rt_renderer* r, const void* spheres48, uint32_t n) {
 int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uint32_t n_nodes, const void* tris64,
                uint32_t n_tris, const void* mats32, uint32_t n_mats) {
     if (!r || !sizes) return fail(RT_ERR_ARG, "rt_set_bvh: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     const uint32_t n = sizes[0], m = sizes[1];
     // The kernel reads nodes[i] for i < n and triangles[j] for j < m only; validate so it cannot fault.
     if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
@@ -850,11 +933,15 @@ int rt_get_frame_count(const rt_renderer* r, uint32_t* out) {
 
 int rt_draw(rt_renderer* r) {
     if (!r) return fail(RT_ERR_ARG, "rt_draw: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     return launch_frames(r, 1, r->time, 0);
 }
 
 int rt_draw_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime) {
     if (!r) return fail(RT_ERR_ARG, "rt_draw_frames: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (count == 0) return RT_OK;
     int rc = launch_frames(r, count, time0, dtime);
     if (!rc) r->time = time0 + (count - 1) * dtime;
@@ -863,6 +950,8 @@ int rt_draw_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtim
 
 int rt_read_image(rt_renderer* r, float* out, size_t n_floats) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_read_image: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_read_image: size mismatch");
     HIP_TRY(hipMemcpyAsync(out, r->image.ptr, n_floats * sizeof(float), hipMemcpyDeviceToHost, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
@@ -871,6 +960,8 @@ int rt_read_image(rt_renderer* r, float* out, size_t n_floats) {
 
 int rt_write_image(rt_renderer* r, const float* in, size_t n_floats) {
     if (!r || !in) return fail(RT_ERR_ARG, "rt_write_image: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_write_image: size mismatch");
     HIP_TRY(hipMemcpyAsync(r->image.ptr, in, n_floats * sizeof(float), hipMemcpyHostToDevice, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
@@ -879,6 +970,8 @@ int rt_write_image(rt_renderer* r, const float* in, size_t n_floats) {
 
 int rt_copy_image_to_device(rt_renderer* r, void* dst, size_t n_floats) {
     if (!r || !dst) return fail(RT_ERR_ARG, "rt_copy_image_to_device: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (n_floats != r->image_floats()) return fail(RT_ERR_ARG, "rt_copy_image_to_device: size mismatch");
     HIP_TRY(hipMemcpyAsync(dst, r->image.ptr, n_floats * sizeof(float), hipMemcpyDeviceToDevice, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
@@ -887,12 +980,16 @@ int rt_copy_image_to_device(rt_renderer* r, void* dst, size_t n_floats) {
 
 int rt_reset_frame_count(rt_renderer* r) {
     if (!r) return fail(RT_ERR_ARG, "rt_reset_frame_count: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     r->frame_count = 0;
     return zero_image(r);
 }
 
 int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (!r) return fail(RT_ERR_ARG, "rt_resize: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     r->width = std::max<uint32_t>(1, width);  // renderer.rs:274-275
     r->height = std::max<uint32_t>(1, height);
     if (r->params.row0 >= r->height) r->params.row0 = 0;
@@ -902,12 +999,16 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
 
 int rt_synchronize(rt_renderer* r) {
     if (!r) return fail(RT_ERR_ARG, "rt_synchronize: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     HIP_TRY(hipStreamSynchronize(r->stream));
     return finish_stats(r);
 }
 
 int rt_release_scratch(rt_renderer* r) {
     if (!r) return fail(RT_ERR_ARG, "rt_release_scratch: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (r->timing_pending) {
         const int rc = finish_stats(r);  // the pending draws' counters, and their kernels done
         if (rc) return rc;
@@ -921,6 +1022,8 @@ int rt_release_scratch(rt_renderer* r) {
 
 int rt_get_stats(const rt_renderer* r, rt_stats* out) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_get_stats: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     int rc = finish_stats(const_cast<rt_renderer*>(r));
     if (rc) return rc;
     *out = r->stats;
@@ -929,6 +1032,8 @@ int rt_get_stats(const rt_renderer* r, rt_stats* out) {
 
 int rt_get_raw_counters(const rt_renderer* r, uint64_t* out, int n) {
     if (!r || !out || n < 0) return fail(RT_ERR_ARG, "rt_get_raw_counters: bad argument");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     int rc = finish_stats(const_cast<rt_renderer*>(r));
     if (rc) return rc;
     for (int i = 0; i < n; i++) out[i] = i < RT_RAW_COUNTERS ? r->raw_counters[i] : 0;
@@ -937,6 +1042,8 @@ int rt_get_raw_counters(const rt_renderer* r, uint64_t* out, int n) {
 
 int rt_get_wave_trace(rt_renderer* r, uint64_t* out, size_t n_words) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_get_wave_trace: null");
+    DeviceScope ds(r->device);
+    if (ds.rc) return ds.rc;
     if (n_words > r->wave_trace_words) return fail(RT_ERR_ARG, "rt_get_wave_trace: more words than recorded");
     if (n_words) HIP_TRY(hipMemcpy(out, r->wave_trace.ptr, n_words * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;

@@ -109,7 +109,9 @@ struct KParams {
     uint32_t nslots;              // sphere slots scanned (arrayLength semantics)
     uint32_t npairs;              // ceil(nslots / 2) entries of sph_pairs
     uint32_t n, m;                // bvh_tree_size
-    uint32_t row0, row_step, nrows;
+    // local row kr is global row row0 + (kr / row_block) * row_stride + kr % row_block (row_stride =
+    // row_step * row_block): blocks of row_block rows dealt round-robin (multi-GPU split; rt_params)
+    uint32_t row0, row_step, nrows, row_block, row_stride;
     float* image;                 // nrows x W x 3
     const float4* sph_geo;        // (cx, cy, cz, r*r) per slot
     const SphereAux* sph_aux;     // per slot
@@ -165,6 +167,12 @@ struct KParams {
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot
 // trace back to the kernel's entry, so every use is a fresh s_load (K$) instead of a live SGPR.
 typedef const __attribute__((address_space(4))) KParams* KPtr;
+
+// Global image row of this renderer's local row kr (seed and camera ray use global coordinates).
+__device__ __forceinline__ uint32_t global_row(uint32_t row0, uint32_t row_block, uint32_t row_stride, uint32_t kr) {
+    const uint32_t b = kr / row_block;
+    return row0 + b * row_stride + (kr - b * row_block);
+}
 typedef const __attribute__((address_space(4))) CamDev* CamPtr;
 __device__ __forceinline__ KPtr kargs() {
     const unsigned long long v = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();

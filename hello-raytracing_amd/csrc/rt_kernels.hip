@@ -461,11 +461,11 @@ __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, 
 }
 
 // (p - c) / radius, exact: the host's correctly rounded 1 / radius and two residual corrections
-// (div_rn_mid) where the numerator's magnitude keeps the residuals exact, the IEEE division elsewhere (zero,
+// (div_rn_mid) where both operands lie in its proven range [2^-60, 2^60], the IEEE division elsewhere (zero,
 // tiny or huge components, radius outside [2^-60, 2^60]: inv_radius = 0).
 __device__ __forceinline__ float div_by_radius(float x, float radius, float inv_radius) {
     const float ax = __builtin_fabsf(x);
-    if (inv_radius != 0.0f && ax >= 0x1p-100f && ax <= 0x1p60f) return div_rn_mid(x, RcpRN{radius, inv_radius});
+    if (inv_radius != 0.0f && ax >= 0x1p-60f && ax <= 0x1p60f) return div_rn_mid(x, RcpRN{radius, inv_radius});
     return x / radius;
 }
 
@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
             B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             if (B.pr_ok) {
-                const uint32_t y = P.row0 + kr * P.row_step;
+                const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
                 const Ray pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
                 B.pr_o = pr.o;
                 B.pr_d = pr.d;
@@ -1342,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool valid = x < P.W && kr < P.nrows;
-    const uint32_t y = P.row0 + kr * P.row_step;
+    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
     float* px = P.image + ((size_t)kr * P.W + x) * 3u;
 
     float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
@@ -1554,7 +1554,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
                 need = false;
                 if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
-                    const uint32_t y = P.row0 + kr * P.row_step;
+                    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
                     ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (job_f0 + (sid >> 6)) * P.dtime, s);
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
@@ -1688,7 +1688,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
             uint32_t ps = 0;
             if (pok) {
-                const uint32_t y = K->row0 + kr * K->row_step;
+                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
                 pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
             }
             blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
@@ -1795,8 +1795,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
                 uint32_t ps = 0;
                 if (pok) {
-                    const uint32_t y = P.row0 + kr * P.row_step;
-                    pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (job_f0 + blk_f) * P.dtime, ps);
+                    const KPtr K = kargs();  // row map and time: loaded here, not held in SGPRs
+                    const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
+                    pr = primary_ray<MODE>(&K->cam, x, y, K->time0 + (job_f0 + blk_f) * K->dtime, ps);
                 }
                 blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
                 blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
@@ -2136,8 +2137,11 @@ hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned lo
 
 // Demangled-symbol form of the kernel a draw ran ("k_trace_split<true>"): rt_stats.kernel, and the key
 // bench.py matches against rocprofv3 summaries.
-static char g_kernel_name[64] = "";
+// Per host thread (renderers driven from several threads each see their own launch); renderer.cpp copies it
+// into the renderer's stats right after its launches and clears it before them.
+static thread_local char g_kernel_name[64] = "";
 const char* hrt_last_kernel() { return g_kernel_name; }
+void hrt_reset_last_kernel() { g_kernel_name[0] = '\0'; }
 static const char* kname(const char* base, int a, int b = -1, int c = -1) {
     if (b < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s>", base, a ? "true" : "false");
     else if (c < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d>", base, a, b);

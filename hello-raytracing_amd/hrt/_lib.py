@@ -26,6 +26,7 @@ RT_MODE_SPHERE = 0
 RT_MODE_TRIS = 1
 RT_MODE_MIXED = 2
 RT_SCHEDULE_AUTO, RT_SCHEDULE_TILES, RT_SCHEDULE_QUEUE = 0, 1, 2
+RT_FOLD_AUTO, RT_FOLD_BUFFER, RT_FOLD_RING = 0, 1, 2
 
 
 class RtParams(C.Structure):
@@ -42,6 +43,10 @@ class RtParams(C.Structure):
         ("job_frames", C.c_uint32),
         ("tri_bvh", C.c_uint32),
         ("suspend_below", C.c_uint32),
+        ("row_block", C.c_uint32),
+        ("fold", C.c_uint32),
+        ("ring_slots_max", C.c_uint32),
+        ("fail_alloc_above_mb", C.c_uint32),
     ]
 
 
@@ -65,6 +70,7 @@ class RtStats(C.Structure):
         ("fold_bytes", C.c_uint64),
         ("fold_ring", C.c_uint32),
         ("pad_stats", C.c_uint32),
+        ("device_bytes", C.c_uint64),
     ]
 
 

@@ -339,8 +339,10 @@ class Renderer:
 
     @property
     def local_rows(self) -> int:
+        from .parallel import local_rows
+
         p = self.params
-        return 0 if p.row0 >= self.height else (self.height - p.row0 + p.row_step - 1) // p.row_step
+        return local_rows(p.row0, p.row_step, self.height, p.row_block)
 
     def read_image(self) -> np.ndarray:
         """copy_image_buffer (render_ppm.rs:7-36): (local_rows, width, 3) float32."""

@@ -17,7 +17,9 @@
  *   Node     32 B  {bound_min: vec4<f32>; bound_max: vec4<f32>}                          src/scene/bvh/node.rs:6-9
  *   Triangle 64 B  {a, b, c: vec4<f32>; custom(normal): vec3<f32>; material: u32}       src/scene/bvh/triangle.rs:7-13
  * The callee copies every input (caller keeps ownership), as wgpu's queue.write_buffer does
- * (renderer.rs:350-353). One handle must not be used from two threads at once.
+ * (renderer.rs:350-353). One handle must not be used from two threads at once. A renderer stays on the
+ * GPU that was current when it was created: every call that touches the device makes that GPU current for
+ * its duration and restores the caller's current device before returning.
  */
 #ifndef HRT_H
 #define HRT_H
@@ -58,7 +60,8 @@ typedef struct rt_params {
     uint32_t bounces;          /* BOUNCE_MAX; default 10 (sphere) / 5 (tris, mixed)                     */
     uint32_t ema_cap;          /* SAMPLE_FRAME; default 1000                                          */
     uint32_t min_sphere_slots; /* arrayLength(&scene) floor; default 100 (zero-filled slots traced)    */
-    uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles)   */
+    uint32_t row0, row_step;   /* this renderer owns rows row0, row0+row_step, ... (multi-GPU tiles); with
+                                  row_block > 1 the blocks of row_block rows starting there (below)    */
     uint32_t frames_per_launch;/* frames fused into one kernel launch by rt_draw_frames (default 32)   */
     uint32_t variant;          /* sphere-scan kernel: 0 auto (4 from 32 slots, 3 from 9, else 1), 1 simple,
                                   3 packed + deferred exact candidates, 4 conservative culling BVH;
@@ -85,7 +88,21 @@ typedef struct rt_params {
                                   query runs to completion, k_trace); default 24 (sphere) / 32 (others);
                                   not used by the mixed program with the culling BVH or tri_bvh = 1.
                                   Bit-identical either way                      */
+    uint32_t row_block;        /* rows per block of the row partition (default 1; 0 reads as 1): the renderer
+                                  owns rows row0 + k*row_step*row_block + j, j < row_block, in that order.
+                                  Rank r of N with row_block 8 and row0 = 8r, row_step = N owns whole
+                                  8-row tile rows dealt round-robin (bench.py)            */
+    uint32_t fold;             /* sample queue colour fold: 0 auto (by queue_budget_mb, above), 1 the sample
+                                  buffer + k_accumulate, 2 the fold ring (bounded memory); bit-identical */
+    uint32_t ring_slots_max;   /* fold ring: at most this many job slots (a power of two; 0 = no cap).
+                                  Tests: with few slots nearly every job waits for one                    */
+    uint32_t fail_alloc_above_mb; /* fault injection for tests: colour-fold allocations above this many MiB
+                                  fail as a refused hipMalloc would (0 = off); the draw then shrinks them */
 } rt_params;
+
+#define RT_FOLD_AUTO 0u
+#define RT_FOLD_BUFFER 1u
+#define RT_FOLD_RING 2u
 
 #define RT_SCHEDULE_AUTO 0u
 #define RT_SCHEDULE_TILES 1u
@@ -115,6 +132,8 @@ typedef struct rt_stats {
     uint32_t fold_ring;    /* 1: the last draw folded through the fold ring (bounded memory), 0: through the
                               sample buffer and k_accumulate (rt_params.queue_budget_mb decides)         */
     uint32_t pad_stats;
+    uint64_t device_bytes; /* device memory the renderer holds after the last draw call (image, scene,
+                              colour fold, counters): the fold's share stays within queue_budget_mb      */
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),
@@ -144,7 +163,9 @@ int rt_get_frame_count(const rt_renderer *r, uint32_t *out);
  * frame_count += 1. Asynchronous on the renderer's HIP stream. */
 int rt_draw(rt_renderer *r);
 /* `count` frames with time_f = time0 + f*dtime, frame_count advancing by one per frame: bit-identical
- * to count x {rt_set_time(time_f); rt_draw()} (the accumulation runs in registers in-kernel). */
+ * to count x {rt_set_time(time_f); rt_draw()}. The tiles schedule accumulates in registers in-kernel; the
+ * sample queue stores each sample's colour (sample buffer or fold ring) and folds them in frame order with
+ * the same expression (k_accumulate after the launch, or inside it), see rt_params.fold. */
 int rt_draw_frames(rt_renderer *r, uint32_t count, uint32_t time0, uint32_t dtime);
 
 /* render_ppm's copy_image_buffer — render_ppm.rs:7-36: blocking readback of the f32 RGB image,

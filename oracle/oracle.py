@@ -21,7 +21,7 @@ MODE_SPHERE, MODE_TRIS, MODE_MIXED = 0, 1, 2
 class OParams(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("width", "height", "mode", "bounces", "ema_cap", "frame0", "time0",
                                           "dtime", "frames", "x0", "nx", "row0", "row_step", "nrows",
-                                          "step_cap")]
+                                          "row_block", "step_cap")]
 
 
 _libs: dict = {}
@@ -35,7 +35,7 @@ def lib(contract: int = 0) -> C.CDLL:
     """The oracle library; contract 1-5 = the float-contract study variants (rt_oracle.c ORACLE_CONTRACT)."""
     if contract not in _libs:
         path = LIB if contract == 0 else HERE / "build" / f"liboracle_c{contract}.so"
-        if not path.exists():
+        if not path.exists() or (HERE / "rt_oracle.c").exists() and path.stat().st_mtime < (HERE / "rt_oracle.c").stat().st_mtime:
             subprocess.run(["make", "-s", "-C", os.fspath(HERE), "all" if contract == 0 else "contracts"], check=True)
         L = C.CDLL(os.fspath(path))
         L.oracle_render.restype = C.c_uint64
@@ -44,7 +44,7 @@ def lib(contract: int = 0) -> C.CDLL:
                                     C.POINTER(C.c_uint64)]
         L.oracle_sizeof.restype = C.c_uint32
         L.oracle_sizeof.argtypes = [C.c_int]
-        assert [L.oracle_sizeof(i) for i in range(5)] == [80, 32, 48, 32, 64]
+        assert [L.oracle_sizeof(i) for i in range(6)] == [80, 32, 48, 32, 64, C.sizeof(OParams)]
         _libs[contract] = L
     return _libs[contract]
 
@@ -58,7 +58,8 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
 
     spheres: SPHERE_DTYPE array (zero slots appended up to min_sphere_slots, default 100 in sphere mode
     like the reference's 100-slot buffer); bvh: (sizes, nodes, triangles, materials) from Tree.view().
-    rows: (row0, row_step, nrows) subset of rows (global coordinates), default all rows.
+    rows: (row0, row_step, nrows[, row_block]) subset of rows (global coordinates), default all rows; with
+    row_block b > 1 local row k is row0 + (k // b) * row_step * b + k % b (rt_params.row_block).
     step_cap: the reference walk's 600-step cap (shader_tris.wgsl:274); 0 = uncapped (only to check the
     opt-in SAH triangle walk, which has no cap).
     Returns (image[nrows, nx, 3] float32, queries).
@@ -67,10 +68,10 @@ def render(*, width: int, height: int, mode: int, camera: np.ndarray, frames: in
         bounces = 10 if mode == MODE_SPHERE else 5
     if min_sphere_slots is None:
         min_sphere_slots = 100 if mode == MODE_SPHERE else 0
-    row0, row_step, nrows = rows if rows is not None else (0, 1, height)
+    row0, row_step, nrows, row_block = (tuple(rows) + (1,))[:4] if rows is not None else (0, 1, height, 1)
     nx = width - x0 if nx is None else nx
     p = OParams(width, height, mode, bounces, ema_cap, frame0, time0, dtime, frames, x0, nx, row0, row_step, nrows,
-                step_cap)
+                row_block, step_cap)
     sph_ptr, nslots, keep = None, 0, []
     if mode != MODE_TRIS:
         sp = spheres if spheres is not None else np.zeros(0, dtype=np.uint8)

@@ -80,6 +80,8 @@ typedef struct {
     uint32_t frames;          /* frames drawn by this call                                       */
     uint32_t x0, nx;          /* column window                                                   */
     uint32_t row0, row_step, nrows; /* rows row0 + k*row_step, k < nrows                         */
+    uint32_t row_block;       /* 0/1: rows as above; b > 1: local row k is row0 + (k/b)*row_step*b + k%b
+                                 (the renderer's blocked row partition, rt_params.row_block)          */
     uint32_t step_cap;        /* intersect_all_node step cap: 600 in the reference (shader_tris.wgsl:274);
                                  0 = uncapped, only to check the opt-in SAH walk (non-parity mode)   */
 } o_params;
@@ -361,7 +363,8 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, tnodes, ttris, tcapped)
 #endif
     for (int64_t k = 0; k < (int64_t)p->nrows; k++) {
-        uint32_t y = p->row0 + (uint32_t)k * p->row_step;
+        const uint32_t rb = p->row_block > 1 ? p->row_block : 1;
+        uint32_t y = p->row0 + ((uint32_t)k / rb) * p->row_step * rb + (uint32_t)k % rb;
         uint64_t q[4] = {0, 0, 0, 0};
         for (uint32_t x = p->x0; x < p->x0 + p->nx; x++) {
             float *px = image + ((size_t)k * p->nx + (x - p->x0)) * 3;

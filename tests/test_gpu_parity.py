@@ -8,6 +8,7 @@ Integer outputs (closest-hit query counts) must match exactly.
 """
 import numpy as np
 import pytest
+import torch
 
 import hrt
 import scenes
@@ -204,49 +205,82 @@ def test_sample_queue_chunks_and_tris_mode():
     assert_parity(imgs[1], ref_img, "suzane tris, queue schedule")
 
 
-def _queue_render_in_subprocess(env_extra: dict, scene_expr: str, frames: int, out_name: str, budget_mb: int = 0):
-    """Renders `scene_expr` (a scenes.* SceneDef) under the queue schedule in a child process with extra
-    environment (the fault-injection and slot-cap knobs are read once per process); returns (image, stats)."""
-    import json
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-
-    code = ("import sys, json; sys.path[:0] = ['hello-raytracing_amd', 'tests']; import numpy as np, scenes, hrt\n"
-            f"sd = {scene_expr}; r = scenes.make_renderer(sd)\n"
-            f"r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE{f', queue_budget_mb={budget_mb}' if budget_mb else ''}); "
-            f"r.draw_frames({frames}, 1000, 10)\n"
-            "np.save(sys.argv[1], r.read_image()); st = r.stats()\n"
-            "print(json.dumps({'launches': st.launches, 'fold_bytes': st.fold_bytes, 'fold_ring': st.fold_ring, "
-            "'queries': st.queries}))\n")
-    root = Path(__file__).resolve().parents[1]
-    out = root / "tests" / "output"
-    out.mkdir(exist_ok=True)
-    p = subprocess.run([sys.executable, "-c", code, str(out / out_name)], cwd=root, env=dict(os.environ, **env_extra),
-                       capture_output=True, text=True, timeout=120)
-    assert p.returncode == 0, p.stderr[-2000:]
-    return np.load(out / out_name), json.loads(p.stdout.strip().splitlines()[-1])
+def _queue_render(sd, frames: int, **params):
+    """Renders `sd` under the queue schedule with extra rt_params (fold, budget, slot cap, fault injection);
+    returns (image, stats)."""
+    r = scenes.make_renderer(sd)
+    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **params)
+    r.draw_frames(frames, 1000, 10)
+    return r.read_image(), r.stats()
 
 
 def test_fold_allocation_failure_shrinks_the_launches():
-    """Allocations the device refuses (fault injection: every allocation above 100 MiB fails in a subprocess
-    with HRT_FAIL_ALLOC_ABOVE_MB=100): the sample buffer (512x512 x 100 frames = 315 MB) is halved until it
-    fits (launches of 25 frames); with a 160 MiB budget (under 64 frames of colours) the fold ring (4096 slots
-    x 32 KB) halves its budget until it fits. Both bit-identical to the default draw."""
-    expr = "scenes.golden_scene('metal_materials', 512, 512)"
-    small, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"}, expr, 100, "alloc_small.npy")
-    assert st["fold_ring"] == 0 and st["launches"] == 8 and 0 < st["fold_bytes"] <= 100 << 20, st
-    ring, st = _queue_render_in_subprocess({"HRT_FAIL_ALLOC_ABOVE_MB": "100"}, expr, 100, "alloc_ring.npy",
-                                           budget_mb=160)
-    assert st["fold_ring"] == 1 and 0 < st["fold_bytes"] <= 100 << 20, st
+    """Allocations the device refuses (fault injection, rt_params.fail_alloc_above_mb = 100: every colour-fold
+    allocation above 100 MiB fails): the sample buffer (512x512 x 100 frames = 315 MB) is halved until it fits
+    (launches of 25 frames); with a 160 MiB budget (under 64 frames of colours) the fold ring (4096 slots x
+    32 KB) halves its budget until it fits. Both bit-identical to the default draw."""
     sd = scenes.golden_scene("metal_materials", 512, 512)
+    small, st = _queue_render(sd, 100, fail_alloc_above_mb=100)
+    assert st.fold_ring == 0 and st.launches == 8 and 0 < st.fold_bytes <= 100 << 20, st
+    ring, st = _queue_render(sd, 100, fail_alloc_above_mb=100, queue_budget_mb=160)
+    assert st.fold_ring == 1 and 0 < st.fold_bytes <= 100 << 20, st
+    want, st = _queue_render(sd, 100)
+    assert st.launches == 2 and st.fold_bytes > 100 << 20
+    np.testing.assert_array_equal(small.view(np.uint32), want.view(np.uint32))
+    np.testing.assert_array_equal(ring.view(np.uint32), want.view(np.uint32))
+
+
+def test_fold_memory_follows_the_budget():
+    """a draw through the sample buffer, then draws with a small budget (fold ring) and with the
+    buffer again: each draw's colour memory is its own fold's only, within the budget (rt_stats.device_bytes,
+    every device buffer the renderer holds), and the images stay bit-identical."""
+    sd = scenes.config_c3(320, 192, 64)
     r = scenes.make_renderer(sd)
     r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE)
-    r.draw_frames(100, 1000, 10)
-    assert r.stats().launches == 2 and r.stats().fold_bytes > 100 << 20
-    np.testing.assert_array_equal(small.view(np.uint32), r.read_image().view(np.uint32))
-    np.testing.assert_array_equal(ring.view(np.uint32), r.read_image().view(np.uint32))
+    r.draw_frames(sd.frames, 1000, 10)
+    want = r.read_image()
+    st = r.stats()
+    base = st.device_bytes - st.fold_bytes  # image, scene, counters
+    assert st.fold_ring == 0 and st.fold_bytes == 64 * 40 * 24 * 64 * 12
+    for budget, fold, ring in ((1, 0, 1), (0, hrt.RT_FOLD_BUFFER, 0), (64, hrt.RT_FOLD_RING, 1), (0, 0, 0)):
+        r.reset_frame_count()
+        r.set_params(queue_budget_mb=budget or 32768, fold=fold)
+        r.draw_frames(sd.frames, 1000, 10)
+        np.testing.assert_array_equal(r.read_image().view(np.uint32), want.view(np.uint32))
+        st = r.stats()
+        assert st.fold_ring == ring, (budget, fold)
+        assert st.device_bytes - base <= max(st.fold_bytes, 1) + (1 << 20), (budget, fold, st.device_bytes, base)
+        if budget:
+            assert st.fold_bytes <= (budget << 20) + (1 << 20), (budget, st.fold_bytes)
+
+
+def test_renderer_calls_from_another_thread():
+    """The device is bound per call (the renderer's, whatever the calling thread has current): a renderer
+    created here is drawn, read and destroyed from a second host thread, bit-identical."""
+    import threading
+    sd = scenes.golden_scene("shadow_rendering", 64, 48)
+    sd.frames = 4
+    a = scenes.make_renderer(sd)
+    a.draw_frames(sd.frames, 1000, 10)
+    want = a.read_image()
+    b = scenes.make_renderer(sd)
+    out = {}
+
+    def work():
+        try:
+            b.draw_frames(sd.frames, 1000, 10)
+            out["img"] = b.read_image()
+            out["kernel"] = b.stats().kernel
+            b.close()
+        except Exception as e:  # noqa: BLE001
+            out["err"] = e
+
+    t = threading.Thread(target=work)
+    t.start()
+    t.join(60)
+    assert "err" not in out, out.get("err")
+    np.testing.assert_array_equal(out["img"].view(np.uint32), want.view(np.uint32))
+    assert out["kernel"] == a.stats().kernel
 
 
 @pytest.mark.parametrize("budget_mb", [0, 1])
@@ -269,20 +303,18 @@ def test_release_scratch_then_draw_again(budget_mb):
 
 @pytest.mark.parametrize("slots", [1, 2, 8])
 def test_fold_ring_slot_reuse_bit_identical(slots):
-    """Very few fold-ring slots (HRT_RING_SLOTS_MAX): nearly every job waits in the free queue for a slot to
-    be returned (1 slot: one job at a time). C3 (k_trace_split) and C4 (k_trace_split_tris) at 160x96,
+    """Very few fold-ring slots (rt_params.ring_slots_max): nearly every job waits in the free queue for a slot
+    to be returned (1 slot: one job at a time). C3 (k_trace_split) and C4 (k_trace_split_tris) at 160x96,
     64 frames (two jobs per tile), and C2 (k_trace, four): images bit-identical to the tiles schedule, same
     ray counts."""
-    for expr in ("scenes.config_c3(160, 96, 64)", "scenes.config_c4(160, 96, 64)", "scenes.config_c2(160, 96, 64)"):
-        img, st = _queue_render_in_subprocess({"HRT_RING_SLOTS_MAX": str(slots)}, expr, 64, f"ring_{slots}.npy",
-                                              budget_mb=1)
-        assert st["fold_ring"] == 1 and st["launches"] == 1 and st["fold_bytes"] <= slots * (32 << 10) + (16 << 10), st
-        sd = eval(expr)
+    for sd in (scenes.config_c3(160, 96, 64), scenes.config_c4(160, 96, 64), scenes.config_c2(160, 96, 64)):
+        img, st = _queue_render(sd, 64, ring_slots_max=slots, queue_budget_mb=1)
+        assert st.fold_ring == 1 and st.launches == 1 and st.fold_bytes <= slots * (32 << 10) + (16 << 10), st
         r = scenes.make_renderer(sd)
         r.set_params(schedule=hrt.RT_SCHEDULE_TILES)
         r.draw_frames(64, 1000, 10)
-        np.testing.assert_array_equal(img.view(np.uint32), r.read_image().view(np.uint32), err_msg=expr)
-        assert st["queries"] == r.stats().queries, expr
+        np.testing.assert_array_equal(img.view(np.uint32), r.read_image().view(np.uint32), err_msg=sd.name)
+        assert st.queries == r.stats().queries, sd.name
 
 
 def test_query_count_matches_oracle():
@@ -307,6 +339,18 @@ def test_row_partition_matches_full_image():
         r.set_params(row0=row0, row_step=step)
         r.draw_frames(6, 1000, 10)
         np.testing.assert_array_equal(r.read_image().view(np.uint32), fimg[row0::step].view(np.uint32))
+    # tile-aligned row blocks dealt round-robin (the multi-GPU split of bench.py), under both schedules and
+    # both colour folds; a ragged last block (50 rows) and a block that is not a multiple of the tile height
+    from hrt.parallel import owned_rows
+    for row0, step, block, sched, budget in [(8, 3, 8, 2, 0), (16, 3, 8, 1, 0), (0, 2, 8, 2, 1), (5, 2, 3, 2, 0),
+                                             (40, 2, 8, 0, 0)]:
+        r = scenes.make_renderer(sd)
+        r.set_params(row0=row0, row_step=step, row_block=block, schedule=sched,
+                     **({"queue_budget_mb": budget} if budget else {}))
+        assert r.local_rows == len(owned_rows(row0, step, sd.height, block))
+        r.draw_frames(6, 1000, 10)
+        rows = owned_rows(row0, step, sd.height, block)
+        np.testing.assert_array_equal(r.read_image().view(np.uint32), fimg[rows].view(np.uint32))
 
 
 @pytest.mark.parametrize("schedule", [0, 2])
@@ -456,8 +500,9 @@ def test_suspendable_heap_walk_bit_identical(variant):
 def test_full_size_headline_configs_agree():
     """BASELINE sizes (C3 and C4 at 1920x1080, 8 frames; the bench renders 1024 / 512): the default
     suspendable-walk kernels, plain k_trace and the tiles schedule give the same image bits and ray counts;
-    an 8-way interleaved row partition (the multi-GPU split) reassembles to the full image; and every 90th
-    row matches the CPU oracle bit for bit."""
+    the 8-way partition of bench.py (8-row blocks dealt round-robin) reassembles to the full image with the
+    same total ray count; and every 90th row matches the CPU oracle bit for bit."""
+    from hrt.parallel import assemble, rank_params
     for sd in (scenes.config_c3(1920, 1080, 8), scenes.config_c4(1920, 1080, 8)):
         runs = []
         for params in ({}, {"suspend_below": 0}, {"schedule": hrt.RT_SCHEDULE_TILES}):
@@ -470,16 +515,16 @@ def test_full_size_headline_configs_agree():
         for other, ost in runs[1:]:
             np.testing.assert_array_equal(img.view(np.uint32), other.view(np.uint32))
             assert ost.queries == st.queries
-        parts = []
+        parts, rays = [], 0
         for rank in range(8):
             r = scenes.make_renderer(sd)
-            r.set_params(row0=rank, row_step=8)
+            r.set_params(**rank_params(rank, 8, 8))
             r.draw_frames(sd.frames, 1000, 10)
-            parts.append(r.read_image())
-        full = np.empty_like(img)
-        for rank in range(8):
-            full[rank::8] = parts[rank]
+            parts.append(torch.from_numpy(r.read_image()))
+            rays += r.stats().queries
+        full = assemble(parts, sd.height, 8, block=8).numpy()
         np.testing.assert_array_equal(full.view(np.uint32), img.view(np.uint32))
+        assert rays == st.queries
         ref, _ = scenes.oracle_render(sd, rows=(45, 90, 12))
         assert_parity(img[45::90], ref, f"{sd.name} full size, every 90th row")
 

@@ -34,5 +34,5 @@ def test_bench_self_launches_ranks_and_gathers(world):
     assert out.returncode == 0, out.stderr[-2000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
-    assert res == {"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}",
+    assert res == {"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}", "row_block": 8,
                    "verify_gather_bitwise": True}
