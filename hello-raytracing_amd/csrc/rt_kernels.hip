@@ -195,44 +195,27 @@ __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float
     return (-b - __builtin_sqrtf(disc)) / a2;
 }
 
-#ifndef HRT_SLAB_FMA
-#define HRT_SLAB_FMA 1
-#endif
-#ifndef HRT_SLAB_RCP
-#define HRT_SLAB_RCP 1
-#endif
-
 // 1/d for the slab tests, |d| >= 1e-30 (else +-1e30). v_rcp_f32 (1 ulp) by default: the padding budget
 // covers it (DESIGN.md §Sphere BVH exactness, slab arithmetic).
 __device__ __forceinline__ float robust_inv(float d) {
-#if HRT_SLAB_RCP
     return __builtin_fabsf(d) >= 1e-30f ? __builtin_amdgcn_rcpf(d) : __builtin_copysignf(1e30f, d);
-#else
-    return __builtin_fabsf(d) >= 1e-30f ? 1.0f / d : __builtin_copysignf(1e30f, d);
-#endif
 }
 
 // Per-query slab constants: the box bound b (relative to bvh_rc) enters as t = (b - o' -/+ pad) / d.
 struct Slab {
     f3 inv;     // robust 1/d
-    f3 lo, hi;  // HRT_SLAB_FMA: (-o' - pad) * inv and (-o' + pad) * inv; else -o' - pad and -o' + pad
+    f3 lo, hi;  // (-o' - pad) * inv and (-o' + pad) * inv
 };
 
 // Slab test of the ray against a box padded by `pad` on every side. Visits when the padded box is entered
 // before it is left, not behind the origin, and not beyond the current best t (equality visits: ties must
-// be seen). HRT_SLAB_FMA: one fma per plane, t = fma(b, inv, (-o' -/+ pad) * inv); its rounding error in
+// be seen). One fma per plane, t = fma(b, inv, (-o' -/+ pad) * inv); its rounding error in
 // distance units is <= 3.02 u D (+1 u with v_rcp), inside the 1.02 delta >= 4.08 u D margin the padding leaves.
 __device__ __forceinline__ bool padded_box_hit(const float4 mn, const float4 mx, const Slab& S, float bt,
                                                float& tenter) {
-#if HRT_SLAB_FMA
     const float t0x = __builtin_fmaf(mn.x, S.inv.x, S.lo.x), t1x = __builtin_fmaf(mx.x, S.inv.x, S.hi.x);
     const float t0y = __builtin_fmaf(mn.y, S.inv.y, S.lo.y), t1y = __builtin_fmaf(mx.y, S.inv.y, S.hi.y);
     const float t0z = __builtin_fmaf(mn.z, S.inv.z, S.lo.z), t1z = __builtin_fmaf(mx.z, S.inv.z, S.hi.z);
-#else
-    const float t0x = (mn.x + S.lo.x) * S.inv.x, t1x = (mx.x + S.hi.x) * S.inv.x;
-    const float t0y = (mn.y + S.lo.y) * S.inv.y, t1y = (mx.y + S.hi.y) * S.inv.y;
-    const float t0z = (mn.z + S.lo.z) * S.inv.z, t1z = (mx.z + S.hi.z) * S.inv.z;
-#endif
     const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmax_ieee(fmin_ieee(t0z, t1z), 0.0f));
     const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmin_ieee(fmax_ieee(t0z, t1z), bt));
     tenter = tmin;
@@ -284,9 +267,6 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     const bool finite_o = __builtin_isfinite(r.o.x) && __builtin_isfinite(r.o.y) && __builtin_isfinite(r.o.z);
     if (!(a2 > 0x1p-100f && a2 < 0x1p100f) || !finite_o) {
         Q.full_scan = 1u;
-#ifdef HRT_DEBUG_SPLIT
-        atomicAdd(P.counter + 5, 1ull);
-#endif
         return false;
     }
     Q.full_scan = 0u;
@@ -314,10 +294,8 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     Q.S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
     Q.S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
     Q.S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
-#if HRT_SLAB_FMA
     Q.S.lo = Q.S.lo * Q.S.inv;
     Q.S.hi = Q.S.hi * Q.S.inv;
-#endif
     Q.node = P.bvh_root;
     return true;
 }
@@ -435,10 +413,6 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
     Q.bt = bt;
     Q.bc = bc;
     Q.full_scan |= overflow;
-#ifdef HRT_DEBUG_SPLIT
-    if (overflow) atomicAdd(P.counter + 6, 1ull);
-    if (sp > 12) atomicAdd(P.counter + 7, 1ull);
-#endif
     return finished != 0u;
 }
 
@@ -668,10 +642,8 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
     S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
     S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
     S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
-#if HRT_SLAB_FMA
     S.lo = S.lo * S.inv;
     S.hi = S.hi * S.inv;
-#endif
     uint32_t node = P.tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
     int sp = 0;
     uint32_t overflow = 0u;  // an integer, not an i1 lane mask (see bvh_run)
@@ -970,9 +942,6 @@ __device__ __forceinline__ void fold_session(uint32_t tile, unsigned long long v
             const uint32_t frame0 = K->frame0 + f0;
             uint32_t off = ring_off(slot, 0u, lane, K->jf_log2);
             uint32_t f = 0;
-#ifdef HRT_EXP_NOFOLD
-            f = nf;
-#endif
             for (; f + U <= nf; f += U) {
                 u32x4 c[U];
 #pragma unroll
@@ -1070,11 +1039,7 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
     const uint32_t slot = J.w[WJ_SLOT + (ref >> 16)];  // per-lane entry: an LDS read, not a uniform value
     const uint32_t off = ring_off(slot, ref & 0xFFFFu, pix & 63u, K->jf_log2);
     const u32x4 v = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
-#ifndef HRT_EXP_NOSTORE
     __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16 /* sc1: write-through */);
-#else
-    if (__float_as_uint(c.x) == 0x7FC00001u) __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16);
-#endif
 }
 
 #ifdef HRT_RINGSTAT
@@ -1740,9 +1705,6 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
 // LNODES (small trees: <= LNODE_CAP nodes, depth <= 8): the fp16 nodes are copied into LDS once per
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
-#ifndef HRT_DEFER_DIELECTRIC
-#define HRT_DEFER_DIELECTRIC 0  // k_trace_split: dielectric hits wait for this many in the wave (0: off)
-#endif
 template <bool LNODES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
@@ -1857,51 +1819,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     qs = 2u;
             }
         }
-#if HRT_DEFER_DIELECTRIC
-        const bool walkers = __ballot(have && qs == 1u) != 0ull;
-#endif
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
             tally.lshade++;
             if (first_active_lane()) tally.wshade++;
 #endif
-            bool done = true, defer = false;
-            if ((qs & 15u) == 2u) {  // (qs >> 4: rounds this lane's shading has waited)
+            bool done = true;
+            if (qs == 2u) {
                 float best = FLT_MAX_REF;
                 const int bi = bvh_end(P, ray, Q, best, tally);
-#if HRT_DEFER_DIELECTRIC
-                // a dielectric hit waits (a few rounds at most, and only while lanes still walk) until several
-                // lanes of the wave have one, so the dielectric arm of scatter runs for them together; the
-                // lane's own arithmetic is unchanged (bvh_end is pure when the walk did not fall back)
-                const bool diel = bi >= 0 && Q.full_scan == 0u && P.sph_aux[bi].id != 1u && P.sph_aux[bi].id != 2u;
-                const uint32_t nd = (uint32_t)__popcll(__ballot(diel));
-                defer = diel && walkers && nd < HRT_DEFER_DIELECTRIC && (qs >> 4) < 3u;
-#endif
-                if (!defer) {
-                    queries++;
-                    if (bi >= 0) {
-                        Hit h;
-                        sphere_record(P, ray, bi, best, h);
-                        scatter<MODE>(P, s, ray, h);
-                        att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
-                        bounce++;
-                        done = bounce >= P.bounces;
-                    }
+                queries++;
+                if (bi >= 0) {
+                    Hit h;
+                    sphere_record(P, ray, bi, best, h);
+                    scatter<MODE>(P, s, ray, h);
+                    att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
+                    bounce++;
+                    done = bounce >= P.bounces;
                 }
             }
-            if (defer) {
-                qs += 16u;
-            } else {
-                if (done) {
-                    const float u = 1.0f - sky_t;
-                    const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
-                    const f3 c = att * sky;
-                    ring_store(J, pix, fl, c);
-                    have = false;
-                    fin = true;
-                }
-                qs = 0u;
+            if (done) {
+                const float u = 1.0f - sky_t;
+                const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
+                const f3 c = att * sky;
+                ring_store(J, pix, fl, c);
+                have = false;
+                fin = true;
             }
+            qs = 0u;
         }
         job_account<1>(J, fin, fl, lane);
     }
