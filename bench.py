@@ -270,6 +270,10 @@ def main() -> int:
                     help="sample queue: colour-buffer budget per chunk in MiB (default: the library's)")
     ap.add_argument("--fold", type=int, default=None,
                     help="sample queue colour fold: 0 auto, 1 sample buffer + k_accumulate, 2 fold ring")
+    ap.add_argument("--heap-lds", type=int, default=None,
+                    help="triangle / mixed programs: 0 auto (heap top in LDS when it fits), 1 off")
+    ap.add_argument("--steal", type=int, default=None,
+                    help="sample queue: frame-block work stealing, 0 auto (short launches), 1 off, 2 on")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -341,6 +345,10 @@ def main() -> int:
         extra["queue_budget_mb"] = args.queue_budget_mb
     if args.fold is not None:
         extra["fold"] = args.fold
+    if args.heap_lds is not None:
+        extra["heap_lds"] = args.heap_lds
+    if args.steal is not None:
+        extra["steal"] = args.steal
     knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
                  tri_bvh=args.tri_bvh, **extra)
     r.set_params(**rank_params(rank, world, args.row_block), **knobs)

@@ -170,6 +170,8 @@ struct rt_renderer {
     DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
+    DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
+    uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
@@ -198,7 +200,7 @@ struct rt_renderer {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
-               wave_trace.bytes();
+               wave_trace.bytes() + steal_slots.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
@@ -522,6 +524,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the heap walk
         // of the triangle / mixed programs; not the opt-in SAH walk
         const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
+        // k_trace_split_tris<.., SMALL>: triangle indices fit 16 bits, and the mixed program's sphere walk (culling
+        // BVH, begin phase) fits an 8-entry stack (a path holds at most depth pending siblings; deeper trees would
+        // only fall back to the exact full scan, but keep the 16-entry kernel for them)
+        P.tri_small = (r->mode != RT_MODE_SPHERE && P.m <= 65535u &&
+                       (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
+                          ? 1u : 0u;
         // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for k_trace's
         // cheap sphere scans (C2: 32 costs 3 %); a power of two (the ring's slot layout)
         uint32_t jf = r->params.job_frames ? r->params.job_frames : (split ? 32u : 16u);
@@ -597,6 +605,22 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                             4ull * zero_words + 8ull * ntiles;
         }
         P.queue = r->counter.ptr + 15;
+        // frame-block work stealing (rt_kernels.hip steal_block): the suspendable-walk kernels with the sample
+        // buffer; one slot per resident wave, at most 32 waves per CU
+        // Auto: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job dealt
+        // late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for long
+        // launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 -> 0.88).
+        {
+            const uint64_t chunks0 = (std::min(chunk, count) + jf - 1u) / jf;
+            const uint64_t jobs0 = (uint64_t)ntiles * chunks0;
+            const bool fits = ntiles < (1u << 25) - 1u && chunks0 < 2048u;  // the slot's tile and chunk fields
+            const bool want = r->params.steal == 2u || (r->params.steal == 0u && jobs0 < 16ull * 24u * std::max(r->cus, 1u));
+            P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
+        }
+        P.steal_cap = 32u * std::max(r->cus, 1u);
+        rc = ensure(r->steal_slots, P.steal_cap);
+        if (rc) return rc;
+        P.steal_slots = r->steal_slots.ptr;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
         for (uint32_t done = 0; done < count; done += chunk) {
             P.nframes = std::min(chunk, count - done);
@@ -609,6 +633,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             P.njobs = (unsigned long long)ntiles * P.nchunks;
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
+            if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
             if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
             rc = trace_events(r, r->trace_pairs_pending);
             if (rc) return rc;
@@ -727,6 +752,7 @@ void delete_buffers(rt_renderer* r) {
     r->tb_hnodes.release();
     r->tb_order.release();
     r->counter.release();
+    r->steal_slots.release();
     r->samples.release();
     r->ring.release();
     r->ring_ctl.release();
@@ -759,6 +785,14 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     if (rc) return rc;
     rt_renderer* r = new rt_renderer();
     r->device = dev;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+            delete r;
+            return fail(RT_ERR_DEVICE, "rt_create: hipDeviceGetAttribute(multiprocessor count) failed");
+        }
+        r->cus = (uint32_t)cus;
+    }
     r->mode = mode;
     r->width = width;
     r->height = height;
@@ -827,6 +861,8 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     if (p->suspend_below > 64) return fail(RT_ERR_ARG, "rt_set_params: suspend_below must be 0..64");
     if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
+    if (p->heap_lds > 1) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto or 1 off");
+    if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

@@ -161,7 +161,11 @@ struct KParams {
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
     uint32_t job_frames, nchunks; // frames per job (a job = one tile x job_frames frames), chunks per tile
     uint32_t suspend_below;       // k_trace_split: suspend the walks once fewer lanes than this still walk
-    uint32_t pad_q;
+    uint32_t tri_small;           // k_trace_split_tris<.., SMALL>: 16-bit triangle lists + the heap top in LDS
+    // frame-block work stealing (k_trace_split / k_trace_split_tris with the sample buffer; rt_kernels.hip steal_block)
+    unsigned long long* steal_slots;  // one per wave: (job + 1) << 32 | frames claimed; zeroed per launch
+    uint32_t steal, nwaves;       // on; waves of the launch (launch_persistent)
+    uint32_t steal_cap, pad_s;    // slots allocated (bounds the grid)
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

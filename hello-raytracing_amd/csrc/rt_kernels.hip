@@ -18,6 +18,7 @@
 #include "rt_device.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 using namespace hrt_dev;
 
@@ -460,14 +461,42 @@ __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, in
 }
 
 // intersect_node (shader_tris.wgsl:150-159); inv = 1/d is the same value for every node of a query.
-__device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3& o, const f3& inv) {
-    const float4 mn = P.nodes[2 * i];
-    const float4 mx = P.nodes[2 * i + 1];
+__device__ __forceinline__ bool node_slab(const float4 mn, const float4 mx, const f3& o, const f3& inv) {
     const float t0x = (mn.x - o.x) * inv.x, t0y = (mn.y - o.y) * inv.y, t0z = (mn.z - o.z) * inv.z;
     const float t1x = (mx.x - o.x) * inv.x, t1y = (mx.y - o.y) * inv.y, t1z = (mx.z - o.z) * inv.z;
     const float tmin = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmin_ieee(t0z, t1z));
     const float tmax = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmax_ieee(t0z, t1z));
     return tmin <= tmax && tmax >= 0.0f;
+}
+__device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3& o, const f3& inv) {
+    return node_slab(P.nodes[2 * i], P.nodes[2 * i + 1], o, inv);
+}
+
+// The top of the implicit heap in LDS (k_trace_split_tris<.., SMALL = true>): nodes 1 .. HEAP_TOP - 1, the first
+// eight levels, copied once per workgroup (8 KB). On Suzanne (C4, C5) they take 72 % of the walk's node tests
+// (the oracle's walk, by depth: 2 / 3 / 6 / 7 / 12 / 13 / 13 / 14 % for depths 0-7, 15 / 15 % for 8-9), and every
+// ray starts at the root. Same node bytes, same test.
+constexpr uint32_t HEAP_TOP = 256;
+
+// Wave-uniform: a step reads LDS when every walking lane of the wave is inside the top, else every lane reads
+// L1/L2 (C4 +5.6 %, C5 +4.3 % over no LDS top). Measured and not kept: lanes inside the top from LDS and the others
+// from L1/L2 in the same step, merged by selects (C4 -4.6 %, C5 -2 %): the extra selects, and the wave still waits
+// for the slowest load of the step. The nodes below the top are read through a buffer descriptor: plain global
+// loads in the other arm get merged with the LDS loads into flat loads of a selected pointer.
+template <bool LTOP>
+__device__ __forceinline__ bool node_hit_top(const KParams& P, const float4* __restrict__ top, uint32_t i, const f3& o,
+                                             const f3& inv) {
+    if constexpr (LTOP) {
+        if (__ballot(i >= HEAP_TOP) == 0ull) return node_slab(top[2 * i], top[2 * i + 1], o, inv);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.n * 32u), 0x00020000);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 32u), 0, 0);
+        const f4v b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 32u + 16u), 0, 0);
+        return node_slab(float4{a.x, a.y, a.z, a.w}, float4{b.x, b.y, b.z, b.w}, o, inv);
+    } else {
+        return node_hit(P, i, o, inv);
+    }
 }
 
 // intersect_triangle, Moller-Trumbore (shader_tris.wgsl:161-202): the candidate t, or -1 when the
@@ -575,9 +604,18 @@ __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W
     W.bj = -1;
 }
 
-template <bool SUSPEND>
-__device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand,
-                                         uint32_t below) {
+// Entry k of a lane's deferred-triangle list. The list lives in the lane's words of a 256-lane LDS region (word w
+// of lane t at w * 256 + t) that the mixed program also uses as the lane's 32-bit sphere-walk stack, so 16-bit
+// entries pack two per word of the SAME lane (cand = (uint16_t*)(words + lane)): entries 2w and 2w + 1 are the two
+// halves of word w. (A plain 16-bit stride of 256 would put a lane's entries in other lanes' words: lane 0's
+// entry 1 in lane 128's stack word 0, i.e. in another wave's live sphere stack — the GPU faulted.)
+__device__ __forceinline__ uint32_t list_at(const uint32_t*, uint32_t k) { return k * 256u; }
+__device__ __forceinline__ uint32_t list_at(const uint16_t*, uint32_t k) { return (k >> 1) * 512u + (k & 1u); }
+
+// LT: the deferred-triangle list's entry type (uint16_t when m <= 65535: half the LDS); LTOP: heap top in LDS
+template <bool SUSPEND, typename LT = uint32_t, bool LTOP = false>
+__device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, LT* cand,
+                                         uint32_t below, const float4* __restrict__ top = nullptr) {
     const f3 inv = W.inv;
     const uint32_t n = P.n, m = P.m;
     uint32_t i = W.i, step = W.step, nc = 0u;
@@ -589,7 +627,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
             bool advance = true;
             if (i < n) {
                 tally.nodes++;
-                if (node_hit(P, i, r.o, inv)) {
+                if (node_hit_top<LTOP>(P, top, i, r.o, inv)) {
                     i *= 2u;
                     advance = false;
                 }
@@ -600,7 +638,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
                     advance = false;
                 } else {
                     tally.tris++;
-                    cand[(nc++) * 256u] = j;
+                    cand[list_at(cand, nc++)] = (LT)j;
                 }
             }
             if (advance) {
@@ -610,7 +648,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
             }
             if (++step == 600u) walking = 0u;  // the reference's step cap
         }
-        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
+        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[list_at(cand, k)], best, bj);  // in the order reached
         nc = 0u;
         if (walking == 0u) break;
         if constexpr (SUSPEND) {
@@ -1224,6 +1262,121 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
     }
 }
 
+// ---- Frame-block work stealing (sample buffer; the suspendable-walk kernels; rt_params.steal) ----
+// A job is one 8x8 tile x job_frames frames, and a wave deals its frames one frame block (the tile's 64 pixels in
+// one frame) at a time. A job's cost varies by orders of magnitude across the image (sky: one query per sample;
+// glass and crevices: up to the bounce cap), so once the job queue is drained the launch used to wait for the
+// slowest job dealt last (C4's 8-way split: shares of 24 ms ideal took 33-55 ms). Here each wave publishes its
+// current job in a 64-bit slot and claims its frames with atomicAdd, STEAL_OWN frames at a time (one atomic per
+// frame block cost C3 2 %); a wave that finds the queue drained claims single frames of other waves' jobs the
+// same way. The atomic decides every frame exactly once; a sample's colour goes to its (frame, pixel) place of the
+// sample buffer whichever wave traced it, so the image bits do not change. Slot: (tile + 1) << 39 | chunk << 28 |
+// frames of the job << 16 | frames claimed — everything a thief needs, without a division (renderer.cpp enables
+// stealing for < 2^25 - 1 tiles and < 2^11 chunks; claims stop once a slot reads exhausted, so the 16-bit count
+// stays far below its field's end). Wave state in the WaveJobs words the sample buffer leaves unused: flags (own
+// job, queue drained, lost race), the last victim, and the claimed frames not dealt yet.
+constexpr uint32_t STEAL_OWN = 4;
+constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u;
+enum : uint32_t { WJ_ST = WJ_TILE, WJ_VICTIM = WJ_TILE + 1, WJ_PRIV_F = WJ_TILE + 2, WJ_PRIV_N = WJ_TILE + 3,
+                  WJ_CLAIM_F = WJ_F0, WJ_CLAIM_T = WJ_LIVE };
+
+__device__ __forceinline__ bool slot_open(unsigned long long w) {
+    return (w >> 39) != 0ull && (uint32_t)(w & 0xFFFFu) < (uint32_t)((w >> 16) & 0xFFFu);
+}
+
+// Lane 0, after its claim of up to `want` frames returned the slot's old value v: the claimed frames go to the
+// wave's words (first frame and tile, then the rest as private frames); every lane reads them with claim_read.
+// (Through LDS, not a cross-lane register broadcast: the walk kernels spilled with the latter.)
+__device__ __forceinline__ void claim_publish(const WaveJobs& J, const KPtr K, unsigned long long v, uint32_t want) {
+    if (slot_open(v)) {
+        const uint32_t got = (uint32_t)(v & 0xFFFFu), nf = (uint32_t)((v >> 16) & 0xFFFu);
+        const uint32_t f = ((uint32_t)(v >> 28) & 0x7FFu) * K->job_frames + got;
+        J.w[WJ_CLAIM_F] = f;
+        J.w[WJ_CLAIM_T] = (uint32_t)(v >> 39) - 1u;
+        J.w[WJ_PRIV_F] = f + 1u;
+        J.w[WJ_PRIV_N] = min(want, nf - got) - 1u;
+    } else {
+        J.w[WJ_CLAIM_F] = ~0u;
+    }
+}
+__device__ __forceinline__ bool claim_read(const WaveJobs& J, uint32_t& tile, uint32_t& frame) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    frame = J.get(WJ_CLAIM_F);
+    tile = J.get(WJ_CLAIM_T);
+    return frame != ~0u;
+}
+
+// The cold part (only once the job queue is drained): every wave's slot, 64 at a time, from the last victim on; one
+// claim attempt per 64 slots (a lost race moves on; the next call comes back).
+__device__ __forceinline__ bool steal_scan(const WaveJobs& J, uint32_t lane, uint32_t& tile, uint32_t& frame) {
+    const KPtr K = kargs();
+    unsigned long long* const slots = K->steal_slots;
+    const uint32_t nw = K->nwaves, start = J.get(WJ_VICTIM);
+    for (uint32_t k = 0; k < nw; k += 64u) {
+        uint32_t idx = start + k + lane;
+        idx = idx >= nw ? idx - nw : idx;
+        const unsigned long long m =
+            __ballot(k + lane < nw && slot_open(__hip_atomic_load(slots + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        if (m != 0ull) {
+            const uint32_t vi = uniform(__shfl(idx, __ffsll((long long)m) - 1));
+            if (lane == 0) claim_publish(J, K, atomicAdd(slots + vi, 1ull), 1u);
+            if (claim_read(J, tile, frame)) {
+                J.set(WJ_VICTIM, vi);
+                return true;
+            }
+            J.set(WJ_ST, J.get(WJ_ST) | ST_RETRY);
+        }
+    }
+    return false;
+}
+
+// The wave's next frame block (tile, frame of the launch): a claimed frame not dealt yet, new frames of its own
+// job, the first frames of a new job, or once the queue is drained a frame claimed from another wave's job. false:
+// nothing claimed; then steal_drained() tells whether no frame is left unclaimed anywhere — none can appear (jobs
+// come only from the drained queue), so the caller stops asking — or an open slot was seen whose claim lost a
+// race (ask again later).
+__device__ __forceinline__ bool steal_block(const WaveJobs& J, uint32_t lane, uint32_t& tile, uint32_t& frame) {
+    const uint32_t priv = J.get(WJ_PRIV_N);
+    if (priv != 0u) {
+        frame = J.get(WJ_PRIV_F);
+        tile = J.get(WJ_CLAIM_T);
+        J.set(WJ_PRIV_F, frame + 1u);
+        J.set(WJ_PRIV_N, priv - 1u);
+        return true;
+    }
+    const KPtr K = kargs();
+    unsigned long long* const slots = K->steal_slots;
+    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t st = J.get(WJ_ST);
+    if (st & ST_OWN) {
+        if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)STEAL_OWN), STEAL_OWN);
+        if (claim_read(J, tile, frame)) return true;
+        J.set(WJ_ST, st & ~ST_OWN);
+    }
+    if (!(st & ST_QEMPTY)) {
+        if (lane == 0) {
+            const uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
+            unsigned long long v = 0;
+            if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
+                const uint32_t t = j / K->nchunks, c = j - t * K->nchunks;
+                const uint32_t nf = min(K->job_frames, K->nframes - c * K->job_frames);
+                v = ((unsigned long long)(t + 1u) << 39) | ((unsigned long long)c << 28) | ((unsigned long long)nf << 16);
+                (void)atomicExch(slots + wid, v + STEAL_OWN);
+            }
+            claim_publish(J, K, v, STEAL_OWN);
+        }
+        if (claim_read(J, tile, frame)) {
+            J.set(WJ_ST, ST_OWN);
+            return true;
+        }
+    }
+    J.set(WJ_ST, ST_QEMPTY);  // (clears ST_RETRY)
+    return steal_scan(J, lane, tile, frame);
+}
+__device__ __forceinline__ bool steal_drained(const WaveJobs& J) { return (J.get(WJ_ST) & ST_RETRY) == 0u; }
+
 // Refill with primary rays by frame block (k_trace with the simple sphere scan): when the wave's block
 // (one frame of its job's 8x8 tile) is used up, every lane computes the primary ray of its own pixel for
 // the next frame at once (all lanes busy), and lanes that need a sample fetch one from the block's owner
@@ -1630,7 +1783,7 @@ struct BlockState {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
 };
 
-template <int MODE>
+template <int MODE, bool STEAL>
 __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float4* blk, bool& drained,
                                                  uint32_t lane, unsigned long long below, bool& have,
                                                  uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
@@ -1640,11 +1793,20 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
     while (m != 0ull) {
         if (B.blk_next == 64u) {
             const KPtr K = kargs();  // queue and camera constants: loaded here, not held in SGPRs
-            if (J.dealing()) {
-                B.blk_f++;
-            } else {
-                if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
+            if constexpr (STEAL) {  // one frame block at a time, stolen once the queue is drained (steal_block)
+                if (!steal_block(J, lane, B.job_tile, B.job_f0)) {
+                    drained = steal_drained(J);
+                    break;
+                }
                 B.blk_f = 0;
+                B.job_nf = 1;
+            } else {
+                if (J.dealing()) {
+                    B.blk_f++;
+                } else {
+                    if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
+                    B.blk_f = 0;
+                }
             }
             B.blk_next = 0;
             const uint32_t x = (B.job_tile % K->tiles_w) * 8u + (lane & 7u);
@@ -1705,7 +1867,9 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // 24.5. A stack overflow (BVH deeper than 14 along a path) falls back to the exact full scan.
 // LNODES (small trees: <= LNODE_CAP nodes, depth <= 8): the fp16 nodes are copied into LDS once per
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
-template <bool LNODES>
+// STEAL: frame-block work stealing (sample buffer; renderer.cpp turns it on for launches with few jobs per wave).
+// A separate instantiation: the runtime-switched form cost C3 3 % with stealing off (register allocation).
+template <bool LNODES, bool STEAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
@@ -1744,11 +1908,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         unsigned long long m = __ballot(need);
         while (m != 0ull) {
             if (blk_next == 64u) {
-                if (J.dealing()) {
-                    blk_f++;
-                } else {
-                    if (!job_acquire(J, lane, drained, job_tile, job_f0, job_nf)) break;
+                if constexpr (STEAL) {  // one frame block at a time, stolen once the queue is drained (steal_block)
+                    if (!steal_block(J, lane, job_tile, job_f0)) {
+                        drained = steal_drained(J);
+                        break;
+                    }
                     blk_f = 0;
+                    job_nf = 1;
+                } else {
+                    if (J.dealing()) {
+                        blk_f++;
+                    } else {
+                        if (!job_acquire(J, lane, drained, job_tile, job_f0, job_nf)) break;
+                        blk_f = 0;
+                    }
                 }
                 blk_next = 0;
                 const uint32_t x = (job_tile % P.tiles_w) * 8u + (lane & 7u);
@@ -1886,15 +2059,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // suspends the heap walk once fewer than `suspend_below` lanes are still walking, so lanes whose rays
 // miss the mesh (one node test) do not idle behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s;
 // C5: 6.25 -> 6.55). Bit-identical to k_trace, with the same node/triangle counts.
-template <int MODE, int SCAN>
+// SMALL (m <= 65535, and with the culling BVH a sphere tree of depth <= 8; renderer.cpp decides): the
+// deferred-triangle list holds 16-bit indices and shares its 8 KB with an 8-entry sphere-walk stack, which makes
+// room for the top of the heap in LDS (HEAP_TOP, 8 KB) at the same 6 workgroups per CU.
+template <int MODE, int SCAN, bool SMALL, bool STEAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
     const uint32_t lane = threadIdx.x & 63u;
     // per-lane deferred-triangle list; with the culling BVH also the sphere walk's stack (never live together:
     // the sphere scan finishes in the begin phase)
-    __shared__ uint32_t tri_list[TRI_BATCH * 256];
-    uint32_t* const cand = tri_list + threadIdx.x;
+    typedef typename std::conditional<SMALL, uint16_t, uint32_t>::type LT;
+    constexpr int SPHERE_STACK = SMALL ? 8 : (int)TRI_BATCH;
+    __shared__ uint32_t lane_words[(SMALL ? TRI_BATCH / 2 : TRI_BATCH) * 256];
+    LT* const cand = (LT*)(lane_words + threadIdx.x);  // (list_at: a lane's entries stay in its own words)
+    uint32_t* const sstack = lane_words + threadIdx.x;
+    __shared__ float4 heap_top[SMALL ? 2 * HEAP_TOP : 1];
+    if constexpr (SMALL) {
+        const uint32_t nn = 2u * min(P.n, HEAP_TOP);
+        for (uint32_t t = threadIdx.x; t < nn; t += 256u) heap_top[t] = P.nodes[t];
+        __syncthreads();
+    }
     uint16_t* defer_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
         __shared__ uint16_t defer_cand[(CAND_CAP + 1) * 256];
@@ -1920,7 +2105,7 @@ k_trace_split_tris(const KParams P) {
     int bi = -1;  // sphere winner slot
     HeapWalk W;
     while (true) {
-        refill_block_lds<MODE>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
+        refill_block_lds<MODE, STEAL>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
@@ -1935,7 +2120,7 @@ k_trace_split_tris(const KParams P) {
                 qs = 3u;
             } else {
                 float sb = FLT_MAX_REF;
-                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<(int)TRI_BATCH>(P, ray, sb, cand, tally);
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
@@ -1944,7 +2129,7 @@ k_trace_split_tris(const KParams P) {
             }
         }
         if (have && qs == 3u) {
-            if (heap_run<true>(P, ray, W, tally, cand, suspend_below)) qs = 4u;
+            if (heap_run<true, LT, SMALL>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
         if (have && qs >= 4u) {
             bool done = true;
@@ -2087,6 +2272,15 @@ hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned lo
 static thread_local char g_kernel_name[64] = "";
 const char* hrt_last_kernel() { return g_kernel_name; }
 void hrt_reset_last_kernel() { g_kernel_name[0] = '\0'; }
+static const char* kname_b(const char* base, int a, int b) {  // <bool, bool>
+    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s>", base, a ? "true" : "false", b ? "true" : "false");
+    return g_kernel_name;
+}
+static const char* kname_ii_bb(const char* base, int a, int b, int c, int d) {  // <int, int, bool, bool>
+    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d, %s, %s>", base, a, b, c ? "true" : "false",
+             d ? "true" : "false");
+    return g_kernel_name;
+}
 static const char* kname(const char* base, int a, int b = -1, int c = -1) {
     if (b < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s>", base, a ? "true" : "false");
     else if (c < 0) snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d>", base, a, b);
@@ -2108,9 +2302,22 @@ static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stre
     if (e != hipSuccess) return e;
     const unsigned long long want = (P.njobs + 3ull) / 4ull;  // no more waves than jobs
     const unsigned long long cap = (unsigned long long)std::max(1, per_cu) * (unsigned long long)cus;
-    const dim3 grid((unsigned)std::min(want, cap));
-    hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, P);
+    const dim3 grid((unsigned)std::min(want, std::min(cap, (unsigned long long)(P.steal_cap / 4u))));
+    KParams Q = P;
+    Q.nwaves = grid.x * 4u;  // work stealing: one slot per wave (renderer.cpp zeroes steal_cap of them)
+    hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, Q);
     return hipGetLastError();
+}
+
+// k_trace_split_tris<MODE, SCAN, SMALL, STEAL> by P.tri_small / P.steal
+template <int MODE, int SCAN>
+static hipError_t launch_split_tris(const KParams& P, hipStream_t stream) {
+    const char* base = "k_trace_split_tris";
+    if (P.tri_small)
+        return P.steal ? launch_persistent(k_trace_split_tris<MODE, SCAN, true, true>, P, stream, kname_ii_bb(base, MODE, SCAN, 1, 1))
+                       : launch_persistent(k_trace_split_tris<MODE, SCAN, true, false>, P, stream, kname_ii_bb(base, MODE, SCAN, 1, 0));
+    return P.steal ? launch_persistent(k_trace_split_tris<MODE, SCAN, false, true>, P, stream, kname_ii_bb(base, MODE, SCAN, 0, 1))
+                   : launch_persistent(k_trace_split_tris<MODE, SCAN, false, false>, P, stream, kname_ii_bb(base, MODE, SCAN, 0, 0));
 }
 
 // Sample queue, part 1: trace every sample of the chunk into P.samples.
@@ -2124,11 +2331,11 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
             // Grays/s. (Splitting both walks measured 5.93; an earlier heap-only form with the stack in
             // the LDS block region, 6.05.)
             if constexpr (MODE == MODE_TRIS) {
-                return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream, kname("k_trace_split_tris", MODE, SCAN_SIMPLE));
+                return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
             } else {
-                if (variant == SCAN_SIMPLE) return launch_persistent(k_trace_split_tris<MODE, SCAN_SIMPLE>, P, stream, kname("k_trace_split_tris", MODE, SCAN_SIMPLE));
-                if (variant == SCAN_DEFER) return launch_persistent(k_trace_split_tris<MODE, SCAN_DEFER>, P, stream, kname("k_trace_split_tris", MODE, SCAN_DEFER));
-                return launch_persistent(k_trace_split_tris<MODE, SCAN_BVH>, P, stream, kname("k_trace_split_tris", MODE, SCAN_BVH));
+                if (variant == SCAN_SIMPLE) return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
+                if (variant == SCAN_DEFER) return launch_split_tris<MODE, SCAN_DEFER>(P, stream);
+                return launch_split_tris<MODE, SCAN_BVH>(P, stream);
             }
         }
     }
@@ -2146,8 +2353,13 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_BVH && P.suspend_below > 0u)
-            return P.bvh_lnodes ? launch_persistent(k_trace_split<true>, P, stream, kname("k_trace_split", 1))
-                                : launch_persistent(k_trace_split<false>, P, stream, kname("k_trace_split", 0));
+        {
+            if (P.steal)
+                return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true>, P, stream, kname_b("k_trace_split", 1, 1))
+                                    : launch_persistent(k_trace_split<false, true>, P, stream, kname_b("k_trace_split", 0, 1));
+            return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false>, P, stream, kname_b("k_trace_split", 1, 0))
+                                : launch_persistent(k_trace_split<false, false>, P, stream, kname_b("k_trace_split", 0, 0));
+        }
         return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
     case MODE_TRIS:
         return P.tri_bvh ? launch_trace_mode<MODE_TRIS, true>(variant, P, stream)

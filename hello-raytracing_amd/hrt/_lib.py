@@ -47,6 +47,8 @@ class RtParams(C.Structure):
         ("fold", C.c_uint32),
         ("ring_slots_max", C.c_uint32),
         ("fail_alloc_above_mb", C.c_uint32),
+        ("heap_lds", C.c_uint32),
+        ("steal", C.c_uint32),
     ]
 
 

@@ -98,6 +98,13 @@ typedef struct rt_params {
                                   Tests: with few slots nearly every job waits for one                    */
     uint32_t fail_alloc_above_mb; /* fault injection for tests: colour-fold allocations above this many MiB
                                   fail as a refused hipMalloc would (0 = off); the draw then shrinks them */
+    uint32_t heap_lds;         /* triangle / mixed programs: 0 auto = the top eight levels of the implicit heap
+                                  in LDS with 16-bit triangle lists whenever m <= 65535 (k_trace_split_tris<..,
+                                  true>), 1 off (every node from L1/L2); bit-identical either way          */
+    uint32_t steal;            /* sample queue with the sample buffer, suspendable-walk kernels: frame-block work
+                                  stealing (a wave whose job queue is drained claims single frames of other
+                                  waves' jobs, so no long job trails the launch): 0 auto = on for launches of
+                                  fewer than 16 jobs per resident wave, 1 off, 2 on; bit-identical always  */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u

@@ -93,7 +93,9 @@ def test_culling_bvh_stress_bit_identical():
             kernels.add(k)
         total += ref_q
     assert total > 1e8, total
-    assert {"k_trace_split<true>", "k_trace_split<false>"} <= kernels, kernels
+    # both node placements of the sample-queue kernel ran (nodes in LDS / fp16 nodes from L1/L2), whichever the
+    # work-stealing instantiation (k_trace_split<LNODES, STEAL>)
+    assert {k.split(",")[0] for k in kernels if k.startswith("k_trace_split<")} >= {"k_trace_split<true", "k_trace_split<false"}, kernels
 
 
 def _f32(x):

@@ -497,6 +497,31 @@ def test_suspendable_heap_walk_bit_identical(variant):
         assert all(c == counts[0] for c in counts), counts
 
 
+@pytest.mark.parametrize("jf", [0, 1, 3])
+def test_work_stealing_bit_identical(jf):
+    """Frame-block work stealing (rt_params.steal = 2; auto turns it on for short launches): waves that find the job
+    queue drained claim single frames of other waves' jobs. Images and ray / node / triangle counts equal the
+    draw without stealing and the oracle, for the sphere program (k_trace_split), the triangle and mixed programs
+    (k_trace_split_tris, heap top in LDS or not), ragged jobs (job_frames 1 and 3 of 7 frames) and a row block."""
+    cases = [(scenes.config_c3(136, 80, 7), {}), (scenes.config_c4(120, 72, 7), {}),
+             (scenes.config_c4(120, 72, 7), {"heap_lds": 1}), (scenes.config_c3(136, 80, 7), {"row0": 8, "row_step": 2, "row_block": 8})]
+    for sd, extra in cases:
+        runs = []
+        for steal in (2, 1):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, steal=steal, job_frames=jf, **extra)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            assert st.fold_ring == 0 and st.suspend_below > 0
+            runs.append((r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests, st.box_tests)))
+        np.testing.assert_array_equal(runs[0][0].view(np.uint32), runs[1][0].view(np.uint32), err_msg=sd.name)
+        assert runs[0][1] == runs[1][1], (sd.name, runs[0][1], runs[1][1])
+        if not extra:
+            ref, q = scenes.oracle_render(sd)
+            assert_parity(runs[0][0], ref, f"{sd.name} stealing, job_frames {jf}")
+            assert runs[0][1][0] == q
+
+
 def test_full_size_headline_configs_agree():
     """BASELINE sizes (C3 and C4 at 1920x1080, 8 frames; the bench renders 1024 / 512): the default
     suspendable-walk kernels, plain k_trace and the tiles schedule give the same image bits and ray counts;
