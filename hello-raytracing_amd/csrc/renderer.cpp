@@ -209,6 +209,10 @@ struct rt_renderer {
 #ifndef HRT_LNODES
 #define HRT_LNODES 1
 #endif
+// heap-top configuration of k_trace_split_tris when rt_params.heap_lds = 0 (rt_kernels.hip heap_top_n)
+#ifndef HRT_HEAP_AUTO
+#define HRT_HEAP_AUTO 3u
+#endif
 
 namespace {
 
@@ -527,9 +531,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // k_trace_split_tris<.., SMALL>: triangle indices fit 16 bits, and the mixed program's sphere walk (culling
         // BVH, begin phase) fits an 8-entry stack (a path holds at most depth pending siblings; deeper trees would
         // only fall back to the exact full scan, but keep the 16-entry kernel for them)
-        P.tri_small = (r->mode != RT_MODE_SPHERE && P.m <= 65535u &&
-                       (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
-                          ? 1u : 0u;
+        P.tri_small = 0u;
+        if (r->mode != RT_MODE_SPHERE && P.m <= 65535u &&
+            (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
+            P.tri_small = r->params.heap_lds >= 2u ? r->params.heap_lds - 1u : HRT_HEAP_AUTO;
+        if (variant == hrt_dev::SCAN_DEFER && r->mode == RT_MODE_MIXED && P.tri_small > 1u) P.tri_small = 1u;
         // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for k_trace's
         // cheap sphere scans (C2: 32 costs 3 %); a power of two (the ring's slot layout)
         uint32_t jf = r->params.job_frames ? r->params.job_frames : (split ? 32u : 16u);
@@ -861,7 +867,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     if (p->suspend_below > 64) return fail(RT_ERR_ARG, "rt_set_params: suspend_below must be 0..64");
     if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
-    if (p->heap_lds > 1) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto or 1 off");
+    if (p->heap_lds > 4) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2-4");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();

@@ -318,7 +318,7 @@ __device__ __forceinline__ void load_hnode(const uint4* __restrict__ hn, uint32_
     n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
 }
 
-template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false>
+template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
     const float4* __restrict__ nodes = P.bvh_nodes;
@@ -362,7 +362,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
                 if (hl && hr) {
                     if (sp < STACK) {
-                        stack[sp * 256] = far;
+                        stack[sp * LS] = far;
                         sp++;
                     } else {
                         overflow = 1u;
@@ -373,7 +373,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
                     if (sp < STACK) {
-                        stack[sp * 256] = lfirst ? right : left;
+                        stack[sp * LS] = lfirst ? right : left;
                         sp++;
                     } else {
                         overflow = 1u;
@@ -404,7 +404,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             finished = 1u;
             break;
         }
-        node = stack[(--sp) * 256];
+        node = stack[(--sp) * LS];
         if constexpr (SUSPEND) {
             if ((uint32_t)__popcll(__ballot(1)) < below) break;
         }
@@ -427,11 +427,11 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
-template <int STACK = BVH_STACK, bool H16 = true>
+template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
+    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16, LS>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
     return bvh_end(P, r, Q, best, tally);
 }
 
@@ -483,11 +483,11 @@ constexpr uint32_t HEAP_TOP = 256;
 // from L1/L2 in the same step, merged by selects (C4 -4.6 %, C5 -2 %): the extra selects, and the wave still waits
 // for the slowest load of the step. The nodes below the top are read through a buffer descriptor: plain global
 // loads in the other arm get merged with the LDS loads into flat loads of a selected pointer.
-template <bool LTOP>
+template <uint32_t HT>
 __device__ __forceinline__ bool node_hit_top(const KParams& P, const float4* __restrict__ top, uint32_t i, const f3& o,
                                              const f3& inv) {
-    if constexpr (LTOP) {
-        if (__ballot(i >= HEAP_TOP) == 0ull) return node_slab(top[2 * i], top[2 * i + 1], o, inv);
+    if constexpr (HT > 0) {
+        if (__ballot(i >= HT) == 0ull) return node_slab(top[2 * i], top[2 * i + 1], o, inv);
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.n * 32u), 0x00020000);
         typedef float f4v __attribute__((ext_vector_type(4)));
@@ -609,11 +609,15 @@ __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W
 // entries pack two per word of the SAME lane (cand = (uint16_t*)(words + lane)): entries 2w and 2w + 1 are the two
 // halves of word w. (A plain 16-bit stride of 256 would put a lane's entries in other lanes' words: lane 0's
 // entry 1 in lane 128's stack word 0, i.e. in another wave's live sphere stack — the GPU faulted.)
-__device__ __forceinline__ uint32_t list_at(const uint32_t*, uint32_t k) { return k * 256u; }
-__device__ __forceinline__ uint32_t list_at(const uint16_t*, uint32_t k) { return (k >> 1) * 512u + (k & 1u); }
+// (LS: lanes per workgroup, the region's word stride)
+template <uint32_t LS>
+__device__ __forceinline__ uint32_t list_at(const uint32_t*, uint32_t k) { return k * LS; }
+template <uint32_t LS>
+__device__ __forceinline__ uint32_t list_at(const uint16_t*, uint32_t k) { return (k >> 1) * (2u * LS) + (k & 1u); }
 
-// LT: the deferred-triangle list's entry type (uint16_t when m <= 65535: half the LDS); LTOP: heap top in LDS
-template <bool SUSPEND, typename LT = uint32_t, bool LTOP = false>
+// LT: the deferred-triangle list's entry type (uint16_t when m <= 65535: half the LDS); HT: nodes 1 .. HT - 1 of
+// the heap are in LDS (`top`; 0 = none); LS: lanes per workgroup
+template <bool SUSPEND, typename LT = uint32_t, uint32_t HT = 0, uint32_t LS = 256>
 __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, LT* cand,
                                          uint32_t below, const float4* __restrict__ top = nullptr) {
     const f3 inv = W.inv;
@@ -627,7 +631,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
             bool advance = true;
             if (i < n) {
                 tally.nodes++;
-                if (node_hit_top<LTOP>(P, top, i, r.o, inv)) {
+                if (node_hit_top<HT>(P, top, i, r.o, inv)) {
                     i *= 2u;
                     advance = false;
                 }
@@ -638,7 +642,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
                     advance = false;
                 } else {
                     tally.tris++;
-                    cand[list_at(cand, nc++)] = (LT)j;
+                    cand[list_at<LS>(cand, nc++)] = (LT)j;
                 }
             }
             if (advance) {
@@ -648,7 +652,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
             }
             if (++step == 600u) walking = 0u;  // the reference's step cap
         }
-        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[list_at(cand, k)], best, bj);  // in the order reached
+        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[list_at<LS>(cand, k)], best, bj);  // in the order reached
         nc = 0u;
         if (walking == 0u) break;
         if constexpr (SUSPEND) {
@@ -1348,7 +1352,7 @@ __device__ __forceinline__ bool steal_block(const WaveJobs& J, uint32_t lane, ui
     }
     const KPtr K = kargs();
     unsigned long long* const slots = K->steal_slots;
-    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t st = J.get(WJ_ST);
     if (st & ST_OWN) {
         if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)STEAL_OWN), STEAL_OWN);
@@ -2059,29 +2063,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // suspends the heap walk once fewer than `suspend_below` lanes are still walking, so lanes whose rays
 // miss the mesh (one node test) do not idle behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s;
 // C5: 6.25 -> 6.55). Bit-identical to k_trace, with the same node/triangle counts.
-// SMALL (m <= 65535, and with the culling BVH a sphere tree of depth <= 8; renderer.cpp decides): the
-// deferred-triangle list holds 16-bit indices and shares its 8 KB with an 8-entry sphere-walk stack, which makes
-// room for the top of the heap in LDS (HEAP_TOP, 8 KB) at the same 6 workgroups per CU.
-template <int MODE, int SCAN, bool SMALL, bool STEAL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
+// HL: the heap's top in LDS (renderer.cpp decides: m <= 65535, and with the culling BVH a sphere tree of depth
+// <= 8). 0: none, 256-lane workgroups and 32-bit triangle lists; 1-3: the deferred-triangle list holds 16-bit
+// indices and shares its words with an 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves
+// per SIMD: 1 = nodes 1..255 (8 levels, 8 KB) with 256-lane workgroups, 2 = nodes 1..511 (9 levels, 16 KB) with 512,
+// 3 = nodes 1..991 (almost 10 levels, 31 KB) with 768 (two workgroups per CU: 78 KB each).
+constexpr uint32_t heap_wg(int hl) { return hl == 2 ? 512u : hl == 3 ? 768u : 256u; }
+constexpr uint32_t heap_top_n(int hl) { return hl == 0 ? 0u : hl == 1 ? 256u : hl == 2 ? 512u : 992u; }
+
+template <int MODE, int SCAN, int HL, bool STEAL>
+__global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
+    constexpr uint32_t WGT = heap_wg(HL), HT = heap_top_n(HL);
     const uint32_t lane = threadIdx.x & 63u;
     // per-lane deferred-triangle list; with the culling BVH also the sphere walk's stack (never live together:
     // the sphere scan finishes in the begin phase)
-    typedef typename std::conditional<SMALL, uint16_t, uint32_t>::type LT;
-    constexpr int SPHERE_STACK = SMALL ? 8 : (int)TRI_BATCH;
-    __shared__ uint32_t lane_words[(SMALL ? TRI_BATCH / 2 : TRI_BATCH) * 256];
+    typedef typename std::conditional<(HL > 0), uint16_t, uint32_t>::type LT;
+    constexpr int SPHERE_STACK = HL > 0 ? 8 : (int)TRI_BATCH;
+    __shared__ uint32_t lane_words[(HL > 0 ? TRI_BATCH / 2 : TRI_BATCH) * WGT];
     LT* const cand = (LT*)(lane_words + threadIdx.x);  // (list_at: a lane's entries stay in its own words)
     uint32_t* const sstack = lane_words + threadIdx.x;
-    __shared__ float4 heap_top[SMALL ? 2 * HEAP_TOP : 1];
-    if constexpr (SMALL) {
-        const uint32_t nn = 2u * min(P.n, HEAP_TOP);
-        for (uint32_t t = threadIdx.x; t < nn; t += 256u) heap_top[t] = P.nodes[t];
+    __shared__ float4 heap_top[HL > 0 ? 2 * HT : 1];
+    if constexpr (HL > 0) {
+        const uint32_t nn = 2u * min(P.n, HT);
+        for (uint32_t t = threadIdx.x; t < nn; t += WGT) heap_top[t] = P.nodes[t];
         __syncthreads();
     }
     uint16_t* defer_list = nullptr;
     if constexpr (SCAN == SCAN_DEFER) {
+        static_assert(HL <= 1, "the deferred scan's lists assume 256-lane workgroups");
         __shared__ uint16_t defer_cand[(CAND_CAP + 1) * 256];
         defer_list = defer_cand + threadIdx.x;
     }
@@ -2090,9 +2101,9 @@ k_trace_split_tris(const KParams P) {
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
-    __shared__ float4 blk[2 * 256];  // the wave's frame block (refill_block_lds)
+    __shared__ float4 blk[2 * WGT];  // the wave's frame block (refill_block_lds)
     BlockState B;
-    __shared__ uint32_t wjobs[4 * WJ_WORDS];
+    __shared__ uint32_t wjobs[(WGT / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     bool drained = false;
     Ray ray;
@@ -2120,7 +2131,7 @@ k_trace_split_tris(const KParams P) {
                 qs = 3u;
             } else {
                 float sb = FLT_MAX_REF;
-                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK>(P, ray, sb, sstack, tally);
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
@@ -2129,7 +2140,7 @@ k_trace_split_tris(const KParams P) {
             }
         }
         if (have && qs == 3u) {
-            if (heap_run<true, LT, SMALL>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
+            if (heap_run<true, LT, HT, WGT>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
         if (have && qs >= 4u) {
             bool done = true;
@@ -2276,9 +2287,8 @@ static const char* kname_b(const char* base, int a, int b) {  // <bool, bool>
     snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s>", base, a ? "true" : "false", b ? "true" : "false");
     return g_kernel_name;
 }
-static const char* kname_ii_bb(const char* base, int a, int b, int c, int d) {  // <int, int, bool, bool>
-    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d, %s, %s>", base, a, b, c ? "true" : "false",
-             d ? "true" : "false");
+static const char* kname_iiib(const char* base, int a, int b, int c, int d) {  // <int, int, int, bool>
+    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%d, %d, %d, %s>", base, a, b, c, d ? "true" : "false");
     return g_kernel_name;
 }
 static const char* kname(const char* base, int a, int b = -1, int c = -1) {
@@ -2289,7 +2299,8 @@ static const char* kname(const char* base, int a, int b = -1, int c = -1) {
 }
 
 template <typename K>
-static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stream, const char* /*name*/) {
+static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stream, const char* /*name*/,
+                                    uint32_t wgt = 256) {
     static int cus = 0;
     if (cus == 0) {
         int dev = 0;
@@ -2298,26 +2309,37 @@ static hipError_t launch_persistent(K kernel, const KParams& P, hipStream_t stre
         if (e != hipSuccess) return e;
     }
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, (int)wgt, 0);
     if (e != hipSuccess) return e;
-    const unsigned long long want = (P.njobs + 3ull) / 4ull;  // no more waves than jobs
+    const unsigned long long wpb = wgt / 64u;
+    const unsigned long long want = (P.njobs + wpb - 1ull) / wpb;  // no more waves than jobs
     const unsigned long long cap = (unsigned long long)std::max(1, per_cu) * (unsigned long long)cus;
-    const dim3 grid((unsigned)std::min(want, std::min(cap, (unsigned long long)(P.steal_cap / 4u))));
+    const dim3 grid((unsigned)std::min(want, std::min(cap, (unsigned long long)P.steal_cap / wpb)));
     KParams Q = P;
-    Q.nwaves = grid.x * 4u;  // work stealing: one slot per wave (renderer.cpp zeroes steal_cap of them)
-    hipLaunchKernelGGL(kernel, grid, dim3(256), 0, stream, Q);
+    Q.nwaves = (uint32_t)(grid.x * wpb);  // work stealing: one slot per wave (renderer.cpp zeroes steal_cap of them)
+    hipLaunchKernelGGL(kernel, grid, dim3((unsigned)wgt), 0, stream, Q);
     return hipGetLastError();
 }
 
-// k_trace_split_tris<MODE, SCAN, SMALL, STEAL> by P.tri_small / P.steal
+// k_trace_split_tris<MODE, SCAN, HL, STEAL> by P.tri_small (the heap-top configuration) / P.steal
+template <int MODE, int SCAN, int HL>
+static hipError_t launch_split_tris_hl(const KParams& P, hipStream_t stream) {
+    const char* base = "k_trace_split_tris";
+    return P.steal ? launch_persistent(k_trace_split_tris<MODE, SCAN, HL, true>, P, stream, kname_iiib(base, MODE, SCAN, HL, 1), heap_wg(HL))
+                   : launch_persistent(k_trace_split_tris<MODE, SCAN, HL, false>, P, stream, kname_iiib(base, MODE, SCAN, HL, 0), heap_wg(HL));
+}
 template <int MODE, int SCAN>
 static hipError_t launch_split_tris(const KParams& P, hipStream_t stream) {
-    const char* base = "k_trace_split_tris";
-    if (P.tri_small)
-        return P.steal ? launch_persistent(k_trace_split_tris<MODE, SCAN, true, true>, P, stream, kname_ii_bb(base, MODE, SCAN, 1, 1))
-                       : launch_persistent(k_trace_split_tris<MODE, SCAN, true, false>, P, stream, kname_ii_bb(base, MODE, SCAN, 1, 0));
-    return P.steal ? launch_persistent(k_trace_split_tris<MODE, SCAN, false, true>, P, stream, kname_ii_bb(base, MODE, SCAN, 0, 1))
-                   : launch_persistent(k_trace_split_tris<MODE, SCAN, false, false>, P, stream, kname_ii_bb(base, MODE, SCAN, 0, 0));
+    if constexpr (SCAN == SCAN_DEFER) {  // (its deferred-scan lists assume 256-lane workgroups)
+        return P.tri_small ? launch_split_tris_hl<MODE, SCAN, 1>(P, stream) : launch_split_tris_hl<MODE, SCAN, 0>(P, stream);
+    } else {
+        switch (P.tri_small) {
+        case 1: return launch_split_tris_hl<MODE, SCAN, 1>(P, stream);
+        case 2: return launch_split_tris_hl<MODE, SCAN, 2>(P, stream);
+        case 3: return launch_split_tris_hl<MODE, SCAN, 3>(P, stream);
+        default: return launch_split_tris_hl<MODE, SCAN, 0>(P, stream);
+        }
+    }
 }
 
 // Sample queue, part 1: trace every sample of the chunk into P.samples.

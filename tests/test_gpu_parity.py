@@ -497,6 +497,36 @@ def test_suspendable_heap_walk_bit_identical(variant):
         assert all(c == counts[0] for c in counts), counts
 
 
+def test_heap_top_configs_bit_identical():
+    """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 eight levels with 256-lane workgroups, 3 nine levels
+    with 512, 4 almost ten with 768): the triangle program (Suzanne, the dragon with its capped walks), the mixed
+    program with the linear and the culling-BVH sphere scans; images and ray / node / triangle counts equal across
+    the configurations, with and without work stealing, and the oracle's."""
+    cases = [scenes.config_c4(120, 72, 5)]
+    mixed = scenes.config_c4(96, 64, 4)
+    mixed.spheres = np.concatenate([mixed.spheres] + [scenes.rtiow_spheres()[:60]])  # culling BVH sphere scan
+    cases.append(mixed)
+    for builder, w, h in (("new_suzane", 80, 60), ("new_dragon", 64, 48)):
+        scene = getattr(hrt.SceneTris, builder)(w, h)
+        cases.append(scenes.SceneDef(builder, hrt.RT_MODE_TRIS, w, h, scene.camera, bvh=scene.tris_bvh.view(), frames=4))
+    for sd in cases:
+        runs = []
+        for heap_lds, steal in ((1, 1), (2, 1), (3, 1), (4, 1), (4, 2), (0, 0)):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, heap_lds=heap_lds, steal=steal)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            runs.append((r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests), st.kernel.decode()))
+        kernels = {k for _, _, k in runs}
+        assert len(kernels) >= 5, kernels  # every configuration ran its own instantiation
+        for img, counts, k in runs[1:]:
+            np.testing.assert_array_equal(runs[0][0].view(np.uint32), img.view(np.uint32), err_msg=f"{sd.name} {k}")
+            assert counts == runs[0][1], (sd.name, k, counts, runs[0][1])
+        ref, q = scenes.oracle_render(sd)
+        assert_parity(runs[-1][0], ref, f"{sd.name} heap top (auto)")
+        assert runs[-1][1][0] == q
+
+
 @pytest.mark.parametrize("jf", [0, 1, 3])
 def test_work_stealing_bit_identical(jf):
     """Frame-block work stealing (rt_params.steal = 2; auto turns it on for short launches): waves that find the job
