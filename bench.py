@@ -274,6 +274,7 @@ def main() -> int:
                     help="triangle / mixed programs: 0 auto (heap top in LDS when it fits), 1 off")
     ap.add_argument("--steal", type=int, default=None,
                     help="sample queue: frame-block work stealing, 0 auto (short launches), 1 off, 2 on")
+    ap.add_argument("--tail-split", type=int, default=None, help="sample queue: 0 auto (quarter jobs at the end), 1 off")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -349,6 +350,8 @@ def main() -> int:
         extra["heap_lds"] = args.heap_lds
     if args.steal is not None:
         extra["steal"] = args.steal
+    if args.tail_split is not None:
+        extra["tail_split"] = args.tail_split
     knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
                  tri_bvh=args.tri_bvh, **extra)
     r.set_params(**rank_params(rank, world, args.row_block), **knobs)

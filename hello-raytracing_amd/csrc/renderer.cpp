@@ -637,6 +637,16 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
             P.njobs = (unsigned long long)ntiles * P.nchunks;
+            // Tail split (sample buffer, no stealing): the last ~2 jobs per resident wave are dealt as quarter
+            // jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames a multiple of 4 and
+            // whole chunks only; rt_params.tail_split = 1 turns it off)
+            P.tail_from = 0xFFFFFFFFu;
+            if (!P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
+                r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
+                const unsigned long long k = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
+                P.tail_from = (uint32_t)(P.njobs - k);
+                P.njobs += 3ull * k;
+            }
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
             if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
@@ -869,6 +879,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
     if (p->heap_lds > 4) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2-4");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
+    if (p->tail_split > 1) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto or 1 off");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

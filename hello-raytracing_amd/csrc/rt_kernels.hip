@@ -1179,17 +1179,39 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
     const KPtr K = kargs();
     uint32_t flags = J.get(WJ_FLAGS);
     if (!K->ring_mode) {  // sample buffer: no entries, no slots
-        uint32_t j = 0;
-        if (lane == 0) j = (uint32_t)atomicAdd(K->queue, 1ull);
-        j = uniform(__shfl(j, 0));
-        if (j >= K->njobs) {
+        // lane 0 takes the job and decodes it into the wave's words (WJ_TILE/WJ_F0/WJ_LIVE, unused by the sample
+        // buffer otherwise); every lane reads them back. The launch's last jobs are dealt in quarters (renderer.cpp
+        // tail_from): a job dealt late then ends soon after the queue drains instead of holding the launch for a
+        // whole job (only for whole chunks of a job_frames multiple of 4).
+        if (lane == 0) {
+            uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
+            uint32_t nf = 0;
+            if (j < K->njobs) {
+                uint32_t sub = 0, sub_shift = 0;
+                if (j >= K->tail_from) {
+                    const uint32_t q = j - K->tail_from;
+                    j = K->tail_from + (q >> 2);
+                    sub = q & 3u;
+                    sub_shift = 2;
+                }
+                const uint32_t t = j / K->nchunks, f0 = (j - t * K->nchunks) * K->job_frames;
+                nf = min(K->job_frames, K->nframes - f0) >> sub_shift;
+                J.w[WJ_TILE] = t;
+                J.w[WJ_F0] = f0 + sub * nf;
+            }
+            J.w[WJ_LIVE] = nf;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        job_nf = J.get(WJ_LIVE);
+        if (job_nf == 0u) {
             drained = true;
             return false;
         }
         J.set(WJ_FLAGS, flags | WJ_DEALING);
-        job_tile = j / K->nchunks;
-        job_f0 = (j % K->nchunks) * K->job_frames;
-        job_nf = min(K->job_frames, K->nframes - job_f0);
+        job_tile = J.get(WJ_TILE);
+        job_f0 = J.get(WJ_F0);
         return true;
     }
     if (!(flags & WJ_WAITING)) {

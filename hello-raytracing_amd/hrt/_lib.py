@@ -49,6 +49,7 @@ class RtParams(C.Structure):
         ("fail_alloc_above_mb", C.c_uint32),
         ("heap_lds", C.c_uint32),
         ("steal", C.c_uint32),
+        ("tail_split", C.c_uint32),
     ]
 
 

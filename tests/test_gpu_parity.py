@@ -497,6 +497,27 @@ def test_suspendable_heap_walk_bit_identical(variant):
         assert all(c == counts[0] for c in counts), counts
 
 
+@pytest.mark.parametrize("jf", [4, 8, 32])
+def test_tail_split_bit_identical(jf):
+    """The launch's last jobs dealt as quarter jobs (rt_params.tail_split, the default with the sample buffer when
+    job_frames is a multiple of 4 and divides the launch's frames): images and every work count equal the draw
+    without the split and the oracle, for the sphere program (k_trace_split and k_trace) and the mixed program."""
+    for sd, extra in ((scenes.config_c3(136, 80, 32), {}), (scenes.config_c3(136, 80, 32), {"suspend_below": 0}),
+                      (scenes.config_c4(120, 72, 32), {})):
+        runs = []
+        for tail in (0, 1):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, tail_split=tail, job_frames=jf, steal=1, **extra)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            runs.append((r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests, st.box_tests)))
+        np.testing.assert_array_equal(runs[0][0].view(np.uint32), runs[1][0].view(np.uint32), err_msg=sd.name)
+        assert runs[0][1] == runs[1][1], (sd.name, runs[0][1], runs[1][1])
+    ref, q = scenes.oracle_render(sd)
+    assert_parity(runs[0][0], ref, f"{sd.name} tail split, job_frames {jf}")
+    assert runs[0][1][0] == q
+
+
 def test_heap_top_configs_bit_identical():
     """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 eight levels with 256-lane workgroups, 3 nine levels
     with 512, 4 almost ten with 768): the triangle program (Suzanne, the dragon with its capped walks), the mixed
