@@ -637,11 +637,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             r->last_suspend = P.suspend_below;
             P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
             P.njobs = (unsigned long long)ntiles * P.nchunks;
-            // Tail split (sample buffer, no stealing): the last ~2 jobs per resident wave are dealt as quarter
-            // jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames a multiple of 4 and
-            // whole chunks only; rt_params.tail_split = 1 turns it off)
+            // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
+            // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
+            // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
             P.tail_from = 0xFFFFFFFFu;
-            if (!P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
+            const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
+            if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
                 r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
                 const unsigned long long k = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
                 P.tail_from = (uint32_t)(P.njobs - k);

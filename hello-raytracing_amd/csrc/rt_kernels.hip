@@ -1174,44 +1174,41 @@ __device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uin
 
 // Makes a job current and dealable: fetch one into a free entry and wait for its slot.
 // false: nothing to deal now (queue drained -> `drained`; every entry still in flight; slot still folding).
+// TAIL: the sample buffer's quarter jobs at the end of the launch (renderer.cpp tail_from; k_trace_split only:
+// the decode cost the walk kernels of the other programs 2-6 spilled VGPRs).
+template <bool TAIL = false>
 __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bool& drained, uint32_t& job_tile,
                                             uint32_t& job_f0, uint32_t& job_nf) {
     const KPtr K = kargs();
     uint32_t flags = J.get(WJ_FLAGS);
     if (!K->ring_mode) {  // sample buffer: no entries, no slots
-        // lane 0 takes the job and decodes it into the wave's words (WJ_TILE/WJ_F0/WJ_LIVE, unused by the sample
-        // buffer otherwise); every lane reads them back. The launch's last jobs are dealt in quarters (renderer.cpp
-        // tail_from): a job dealt late then ends soon after the queue drains instead of holding the launch for a
-        // whole job (only for whole chunks of a job_frames multiple of 4).
-        if (lane == 0) {
-            uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
-            uint32_t nf = 0;
-            if (j < K->njobs) {
-                uint32_t sub = 0, sub_shift = 0;
-                if (j >= K->tail_from) {
-                    const uint32_t q = j - K->tail_from;
-                    j = K->tail_from + (q >> 2);
-                    sub = q & 3u;
-                    sub_shift = 2;
-                }
-                const uint32_t t = j / K->nchunks, f0 = (j - t * K->nchunks) * K->job_frames;
-                nf = min(K->job_frames, K->nframes - f0) >> sub_shift;
-                J.w[WJ_TILE] = t;
-                J.w[WJ_F0] = f0 + sub * nf;
-            }
-            J.w[WJ_LIVE] = nf;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        job_nf = J.get(WJ_LIVE);
-        if (job_nf == 0u) {
+        uint32_t j = 0;
+        if (lane == 0) j = (uint32_t)atomicAdd(K->queue, 1ull);
+        j = uniform(__shfl(j, 0));
+        if (j >= K->njobs) {
             drained = true;
             return false;
         }
         J.set(WJ_FLAGS, flags | WJ_DEALING);
-        job_tile = J.get(WJ_TILE);
-        job_f0 = J.get(WJ_F0);
+        if constexpr (TAIL) {
+            // The launch's last jobs are dealt in quarters: a job dealt late then ends soon after the queue
+            // drains instead of holding the launch for a whole job (whole chunks of a job_frames multiple of 4)
+            const uint32_t tail = K->tail_from;
+            const bool quarter = j >= tail;
+            const uint32_t q = j - tail;
+            const uint32_t jj = quarter ? tail + (q >> 2) : j;
+            job_tile = jj / K->nchunks;
+            job_f0 = (jj - job_tile * K->nchunks) * K->job_frames;
+            job_nf = min(K->job_frames, K->nframes - job_f0);
+            if (quarter) {
+                job_nf >>= 2;
+                job_f0 += (q & 3u) * job_nf;
+            }
+        } else {
+            job_tile = j / K->nchunks;
+            job_f0 = (j % K->nchunks) * K->job_frames;
+            job_nf = min(K->job_frames, K->nframes - job_f0);
+        }
         return true;
     }
     if (!(flags & WJ_WAITING)) {
@@ -1945,7 +1942,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     if (J.dealing()) {
                         blk_f++;
                     } else {
-                        if (!job_acquire(J, lane, drained, job_tile, job_f0, job_nf)) break;
+                        if (!job_acquire<true>(J, lane, drained, job_tile, job_f0, job_nf)) break;
                         blk_f = 0;
                     }
                 }
@@ -2394,6 +2391,9 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
 
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {
     if (P.njobs == 0) return hipSuccess;
+    // quarter jobs (tail_from) are decoded by k_trace_split only (job_acquire<TAIL>)
+    if (P.tail_from != 0xFFFFFFFFu && !(mode == MODE_SPHERE && variant == SCAN_BVH && P.suspend_below > 0u && !P.steal))
+        return hipErrorInvalidValue;
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_BVH && P.suspend_below > 0u)

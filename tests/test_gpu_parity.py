@@ -499,9 +499,9 @@ def test_suspendable_heap_walk_bit_identical(variant):
 
 @pytest.mark.parametrize("jf", [4, 8, 32])
 def test_tail_split_bit_identical(jf):
-    """The launch's last jobs dealt as quarter jobs (rt_params.tail_split, the default with the sample buffer when
+    """The launch's last jobs dealt as quarter jobs (rt_params.tail_split: k_trace_split with the sample buffer when
     job_frames is a multiple of 4 and divides the launch's frames): images and every work count equal the draw
-    without the split and the oracle, for the sphere program (k_trace_split and k_trace) and the mixed program."""
+    without the split and the oracle; k_trace (suspend_below 0) and the mixed program ignore the knob."""
     for sd, extra in ((scenes.config_c3(136, 80, 32), {}), (scenes.config_c3(136, 80, 32), {"suspend_below": 0}),
                       (scenes.config_c4(120, 72, 32), {})):
         runs = []
