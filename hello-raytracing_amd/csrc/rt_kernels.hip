@@ -1876,6 +1876,40 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
     }
 }
 
+#ifdef HRT_PHASES  // diagnostic build (-DHRT_STAMPS -DHRT_PHASES): wave cycles per phase of a round, phase lanes
+#define HRT_PHASE_DECL                                                                       \
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, pl[4] = {0, 0, 0, 0}, pr[4] = {0, 0, 0, 0}; \
+    const unsigned long long ph_start = hrt_stamp();                                         \
+    unsigned long long ph_t = ph_start
+#define HRT_PHASE(k)                                                                         \
+    do {                                                                                     \
+        const unsigned long long t_ = hrt_stamp();                                          \
+        ph[k] += t_ - ph_t;                                                                  \
+        ph_t = t_;                                                                           \
+    } while (0)
+#define HRT_LANES(k, pred)                                                                   \
+    do {                                                                                     \
+        const uint32_t c_ = (uint32_t)__popcll(__ballot(pred));                              \
+        if (c_) { pl[k] += c_; pr[k]++; }                                                    \
+    } while (0)
+// counter[8..11] wave cycles in refill, begin, walk, shade (+ job accounting); [12] wave lifetime cycles;
+// [5] / [6] / [7] lanes summed over the rounds that ran begin / walk / shade, [13] / [14] the rounds that ran
+// begin / shade (phase utilisation = lanes / rounds)
+#define HRT_PHASE_FLUSH                                                                      \
+    if (lane == 0) {                                                                         \
+        for (int k = 0; k < 4; k++) atomicAdd(P.counter + 8 + k, ph[k]);                     \
+        atomicAdd(P.counter + 12, hrt_stamp() - ph_start);                                   \
+        for (int k = 0; k < 3; k++) atomicAdd(P.counter + 5 + k, pl[k]);                     \
+        atomicAdd(P.counter + 13, pr[0]);                                                    \
+        atomicAdd(P.counter + 14, pr[2]);                                                    \
+    }
+#else
+#define HRT_PHASE_DECL do { } while (0)
+#define HRT_PHASE(k) do { } while (0)
+#define HRT_LANES(k, pred) do { } while (0)
+#define HRT_PHASE_FLUSH
+#endif
+
 // Sample queue with suspendable walks (sphere program, culling BVH; rt_params.suspend_below > 0).
 // In k_trace a wave's query step lasts as long as its slowest lane's walk: secondary rays of one wave
 // take very different paths through the tree, so most lanes idle at the end of every step (PMC of
@@ -1926,6 +1960,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
     __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
+    HRT_PHASE_DECL;
     while (true) {
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
@@ -2000,6 +2035,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #ifdef HRT_STAMPS
         if (lane == 0) tally.rounds++;
 #endif
+        HRT_PHASE(0);
+        HRT_LANES(0, have && qs == 0u);
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
                 qs = bvh_begin<true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
@@ -2007,6 +2044,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 qs = 3u;
             }
         }
+        HRT_PHASE(1);
+        HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
             if constexpr (LNODES) {
                 if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
@@ -2015,6 +2054,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     qs = 2u;
             }
         }
+        HRT_PHASE(2);
+        HRT_LANES(2, have && qs >= 2u);
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
             tally.lshade++;
@@ -2045,8 +2086,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             qs = 0u;
         }
         job_account<1>(J, fin, fl, lane);
+        HRT_PHASE(3);
     }
-#ifdef HRT_STAMPS
+    HRT_PHASE_FLUSH
+#if defined(HRT_STAMPS) && !defined(HRT_PHASES)
     {
         unsigned long long v[7] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
                                    tally.wshade};
@@ -2134,12 +2177,15 @@ k_trace_split_tris(const KParams P) {
     uint32_t qs = 0;
     int bi = -1;  // sphere winner slot
     HeapWalk W;
+    HRT_PHASE_DECL;
     while (true) {
         refill_block_lds<MODE, STEAL>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
         }
+        HRT_PHASE(0);
+        HRT_LANES(0, have && qs == 0u);
         bool fin = false;
         if (have && qs == 0u) {
             if (bounce >= P.bounces) {
@@ -2158,9 +2204,13 @@ k_trace_split_tris(const KParams P) {
                 qs = 3u;
             }
         }
+        HRT_PHASE(1);
+        HRT_LANES(1, have && qs == 3u);
         if (have && qs == 3u) {
             if (heap_run<true, LT, HT, WGT>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
+        HRT_PHASE(2);
+        HRT_LANES(2, have && qs >= 4u);
         if (have && qs >= 4u) {
             bool done = true;
             if (qs == 4u) {
@@ -2188,7 +2238,9 @@ k_trace_split_tris(const KParams P) {
             qs = 0u;
         }
         job_account<SCAN == SCAN_BVH ? 1 : 2>(J, fin, fl, lane);
+        HRT_PHASE(3);
     }
+    HRT_PHASE_FLUSH
 #ifdef HRT_RINGSTAT
     if (lane == 0)
         for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
