@@ -61,13 +61,15 @@ struct Hit {
 // intersect_all_sphere + intersect_sphere (shader_sphere.wgsl:218-229, :136-155). Returns the slot of
 // the closest root with t > 0 && t < best (first slot wins ties), or -1. Skipping b >= 0 is exact:
 // then -b - sqrt(disc) <= 0, so t <= 0 (or NaN) and the reference rejects it too.
-__device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, float& best) {
+// (PP: a KParams pointer, generic or the kernarg segment's constant one: kargs())
+template <typename PP>
+__device__ __forceinline__ int scan_spheres_p(PP P, const Ray& r, float& best) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a;
     const float a2 = 2.0f * a;
     int bi = -1;
-    const float4* __restrict__ geo = P.sph_geo;
-    const uint32_t ns = P.nslots;
+    const float4* __restrict__ geo = P->sph_geo;
+    const uint32_t ns = P->nslots;
     for (uint32_t i = 0; i < ns; i++) {
         const float4 g = geo[i];  // wave-uniform: scalar load
         const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
@@ -83,6 +85,9 @@ __device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, floa
         }
     }
     return bi;
+}
+__device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, float& best) {
+    return scan_spheres_p(&P, r, best);
 }
 
 // The reference's t for slot i, recomputed exactly as the scan computes it (scalar IEEE ops give the
@@ -260,7 +265,7 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 }
 
 // Returns true when the walk has to run (false: bvh_end does the full scan).
-template <bool H16 = false, bool FAST = false>
+template <bool H16 = false, bool FAST = false, bool KA = false>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -276,12 +281,13 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     const uint32_t nleaf = P.bvh_nleaf;
     float bt = best;
     int bc = -1;
-    for (uint32_t k = 0; k < P.nlarge; k++) {  // ascending slots: a later equal t never wins here
+    const uint32_t nlarge = KA ? kargs()->nlarge : P.nlarge;  // (KA: loaded per query, not held in SGPRs)
+    for (uint32_t k = 0; k < nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
         const float t = exact_t_geo<FAST>(P.sph_geo[i], r, a4, a2);
         if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
-    tally.spheres += P.nlarge;
+    tally.spheres += nlarge;
     Q.bt = bt;
     Q.bc = bc;
 
@@ -417,9 +423,16 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
     return finished != 0u;
 }
 
+// KA: the fallback scan reads its constants through kargs() (k_trace_split: no SGPRs held for the rare path)
+template <bool KA = false>
 __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const BvhQuery& Q, float& best,
                                        Tally& tally) {
     if (Q.full_scan != 0u) {
+        if constexpr (KA) {
+            const KPtr K = kargs();
+            tally.spheres += K->nslots;
+            return scan_spheres_p(K, r, best);
+        }
         tally.spheres += P.nslots;
         return scan_spheres(P, r, best);
     }
@@ -2039,7 +2052,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(0, have && qs == 0u);
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
-                qs = bvh_begin<true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+                qs = bvh_begin<true, true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
             } else {  // bounce cap 0: the sample is the sky colour
                 qs = 3u;
             }
@@ -2064,7 +2077,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             bool done = true;
             if (qs == 2u) {
                 float best = FLT_MAX_REF;
-                const int bi = bvh_end(P, ray, Q, best, tally);
+                const int bi = bvh_end<true>(P, ray, Q, best, tally);
                 queries++;
                 if (bi >= 0) {
                     Hit h;
@@ -2113,9 +2126,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
     if (lane == 0) {
+        unsigned long long* const cnt = kargs()->counter;  // (loaded here, not held in SGPRs)
 #pragma unroll
         for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+            if (sums[c]) atomicAdd(cnt + c, sums[c]);
     }
 }
 
