@@ -528,11 +528,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // suspendable walks (k_trace_split / k_trace_split_tris): the sphere program's culling BVH, the heap walk
         // of the triangle / mixed programs; not the opt-in SAH walk
         const bool split = !P.tri_bvh && (r->mode != RT_MODE_SPHERE || variant == hrt_dev::SCAN_BVH);
-        // k_trace_split_tris<.., SMALL>: triangle indices fit 16 bits, and the mixed program's sphere walk (culling
-        // BVH, begin phase) fits an 8-entry stack (a path holds at most depth pending siblings; deeper trees would
-        // only fall back to the exact full scan, but keep the 16-entry kernel for them)
+        // k_trace_split_tris<.., HL > 0> (heap top in LDS, 8 leaf-pair list words per lane): the mixed program's
+        // sphere walk (culling BVH, begin phase) fits an 8-entry stack (a path holds at most depth pending siblings;
+        // deeper trees would only fall back to the exact full scan, but keep the 16-entry kernel for them)
         P.tri_small = 0u;
-        if (r->mode != RT_MODE_SPHERE && P.m <= 65535u &&
+        if (r->mode != RT_MODE_SPHERE &&
             (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
             P.tri_small = r->params.heap_lds >= 2u ? r->params.heap_lds - 1u : HRT_HEAP_AUTO;
         if (variant == hrt_dev::SCAN_DEFER && r->mode == RT_MODE_MIXED && P.tri_small > 1u) P.tri_small = 1u;
@@ -922,6 +922,9 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
     if ((n && !nodes32) || (m && !tris64) || (n_mats && !mats32)) return fail(RT_ERR_ARG, "rt_set_bvh: null buffer");
     if (n > (1u << 30)) return fail(RT_ERR_ARG, "rt_set_bvh: tree too large");
+    // Tree::build (tree.rs:38) makes n = m.next_power_of_two() (>= 1); the walks rely on it (leaf pairs: the
+    // children of nodes n/2 .. n-1 are leaves)
+    if (n == 0 || (n & (n - 1u)) != 0) return fail(RT_ERR_ARG, "rt_set_bvh: sizes[0] must be a power of two");
     if (n_mats >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_bvh: more than 2^28 materials");
     const hrt::Triangle* T = (const hrt::Triangle*)tris64;
     std::vector<hrt_dev::TriDev> td(m);

@@ -485,11 +485,10 @@ __device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3&
     return node_slab(P.nodes[2 * i], P.nodes[2 * i + 1], o, inv);
 }
 
-// The top of the implicit heap in LDS (k_trace_split_tris<.., SMALL = true>): nodes 1 .. HEAP_TOP - 1, the first
-// eight levels, copied once per workgroup (8 KB). On Suzanne (C4, C5) they take 72 % of the walk's node tests
-// (the oracle's walk, by depth: 2 / 3 / 6 / 7 / 12 / 13 / 13 / 14 % for depths 0-7, 15 / 15 % for 8-9), and every
-// ray starts at the root. Same node bytes, same test.
-constexpr uint32_t HEAP_TOP = 256;
+// The top of the implicit heap in LDS (k_trace_split_tris<.., HL > 0>): nodes 1 .. HT - 1, copied once per
+// workgroup. On Suzanne (C4, C5) the first eight levels take 72 % of the walk's node tests (the oracle's walk, by
+// depth: 2 / 3 / 6 / 7 / 12 / 13 / 13 / 14 % for depths 0-7, 15 / 15 % for 8-9), and every ray starts at the root.
+// Same node bytes, same test.
 
 // Wave-uniform: a step reads LDS when every walking lane of the wave is inside the top, else every lane reads
 // L1/L2 (C4 +5.6 %, C5 +4.3 % over no LDS top). Measured and not kept: lanes inside the top from LDS and the others
@@ -617,61 +616,86 @@ __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W
     W.bj = -1;
 }
 
-// Entry k of a lane's deferred-triangle list. The list lives in the lane's words of a 256-lane LDS region (word w
-// of lane t at w * 256 + t) that the mixed program also uses as the lane's 32-bit sphere-walk stack, so 16-bit
-// entries pack two per word of the SAME lane (cand = (uint16_t*)(words + lane)): entries 2w and 2w + 1 are the two
-// halves of word w. (A plain 16-bit stride of 256 would put a lane's entries in other lanes' words: lane 0's
-// entry 1 in lane 128's stack word 0, i.e. in another wave's live sphere stack — the GPU faulted.)
-// (LS: lanes per workgroup, the region's word stride)
-template <uint32_t LS>
-__device__ __forceinline__ uint32_t list_at(const uint32_t*, uint32_t k) { return k * LS; }
-template <uint32_t LS>
-__device__ __forceinline__ uint32_t list_at(const uint16_t*, uint32_t k) { return (k >> 1) * (2u * LS) + (k & 1u); }
+// Leaf pairs. A bottom node i (n/2 <= i < n) has the leaves 2i and 2i + 1 as children, and when the reference's
+// walk hits it, its next two loop bodies are exactly those leaves (2i is even, so the walk steps to 2i + 1), after
+// which it climbs from 2i + 1, i.e. from i: (2i + 1) >> ctz(~(2i + 1)) = i >> ctz(~i). So one loop iteration here
+// is one node test, and a hit bottom node appends both its leaves to the deferred list as one entry (j0 = 2i - n,
+// PAIR_BIT when j0 + 1 is a triangle too) and advances the step count by the two leaf bodies. Every iteration runs
+// the same node test: no lane sits out a leaf body while the others test nodes (the per-step leaf branch was
+// 17 % of C4's walk steps). Visits, the order of the triangle tests, the 600-step cap (a leaf body the cap cuts
+// off is not run) and the walk's end at the first leaf j >= m are the reference's; so are the node and triangle
+// counts.
+constexpr uint32_t PAIR_BIT = 0x80000000u;
 
-// LT: the deferred-triangle list's entry type (uint16_t when m <= 65535: half the LDS); HT: nodes 1 .. HT - 1 of
-// the heap are in LDS (`top`; 0 = none); LS: lanes per workgroup
-template <bool SUSPEND, typename LT = uint32_t, uint32_t HT = 0, uint32_t LS = 256>
-__device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, LT* cand,
+// HT: nodes 1 .. HT - 1 of the heap are in LDS (`top`; 0 = none); LS: lanes per workgroup, the stride of the
+// lane's list words (`cand` = this lane's first word; entry k at cand[k * LS]); CAP: list entries per lane.
+// (The node count is not kept per iteration: every iteration adds one node test and one step, a pair two steps and
+// two triangles, and an append that ends the walk one of each, so the run's node tests are its steps less its
+// triangles.)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;  // 32-bit LDS addressing for the list
+
+template <bool SUSPEND, uint32_t HT = 0, uint32_t LS = 256, uint32_t CAP = TRI_BATCH>
+__device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand_g,
                                          uint32_t below, const float4* __restrict__ top = nullptr) {
+    // the list's LDS byte address (32-bit arithmetic): entry k at c0 + k * 4 LS
+    const uint32_t c0 = (uint32_t)(uintptr_t)(lds_u32*)cand_g;
     const f3 inv = W.inv;
     const uint32_t n = P.n, m = P.m;
     uint32_t i = W.i, step = W.step, nc = 0u;
+    const uint32_t step0 = step, tris0 = tally.tris;
     uint32_t walking = 1u;  // an integer, not an i1 lane mask (see bvh_run)
     float best = W.best;
     int bj = W.bj;
-    while (true) {
-        while (walking != 0u && __ballot(nc == TRI_BATCH) == 0ull) {
-            bool advance = true;
-            if (i < n) {
-                tally.nodes++;
-                if (node_hit_top<HT>(P, top, i, r.o, inv)) {
-                    i *= 2u;
-                    advance = false;
-                }
-            } else {
-                const uint32_t j = i - n;
-                if (j >= m) {
-                    walking = 0u;
-                    advance = false;
-                } else {
-                    tally.tris++;
-                    cand[list_at<LS>(cand, nc++)] = (LT)j;
-                }
-            }
-            if (advance) {
-                i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
-                if (i == 0u) walking = 0u;
-                i++;
-            }
-            if (++step == 600u) walking = 0u;  // the reference's step cap
+    if (i >= n) {  // n == 1: the root is leaf 0, the walk's only body (heap_begin starts every walk at i = 1)
+        if (m != 0u) {
+            tally.tris++;
+            step++;
+            *(lds_u32*)(uintptr_t)c0 = 0u;
+            nc = 1u;
         }
-        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[list_at<LS>(cand, k)], best, bj);  // in the order reached
+        walking = 0u;
+    }
+    while (true) {
+        while (walking != 0u && __ballot(nc == CAP) == 0ull) {
+            step++;
+            const bool hit = node_hit_top<HT>(P, top, i, r.o, inv);
+            const bool down = hit && 2u * i < n;
+            if (hit && !down) {  // bottom node: the leaf bodies 2i, 2i + 1
+                const uint32_t j0 = 2u * i - n;
+                if (j0 + 2u <= m && step <= 598u) {
+                    tally.tris += 2u;
+                    *(lds_u32*)(uintptr_t)(c0 + __umul24(nc, 4u * LS)) = j0 | PAIR_BIT;
+                    nc++;
+                    step += 2u;
+                } else {  // the cap or the end of the triangles cuts the pair (once per walk at most)
+                    walking = 0u;  // this walk ends within the two leaf bodies (the cap, or j >= m: break)
+                    if (step < 600u && j0 < m) {
+                        tally.tris++;
+                        step++;
+                        *(lds_u32*)(uintptr_t)(c0 + __umul24(nc, 4u * LS)) = j0;
+                        nc++;
+                    }
+                }
+            }
+            const uint32_t ip1 = i + 1u;
+            const uint32_t up = ip1 >> __builtin_ctz(ip1);  // while (i & 1) i /= 2; i++ (1: i was 2^k - 1, the end)
+            if (!down && up == 1u) walking = 0u;
+            i = down ? 2u * i : up;
+            if (step >= 600u) walking = 0u;  // the reference's step cap
+        }
+        for (uint32_t k = 0; k < nc; k++) {  // in the order reached
+            const uint32_t e = *(const lds_u32*)(uintptr_t)(c0 + __umul24(k, 4u * LS));
+            const uint32_t j = e & ~PAIR_BIT;
+            tri_test(P, r, j, best, bj);
+            if (e & PAIR_BIT) tri_test(P, r, j + 1u, best, bj);
+        }
         nc = 0u;
         if (walking == 0u) break;
         if constexpr (SUSPEND) {
             if ((uint32_t)__popcll(__ballot(1)) < below) break;
         }
     }
+    tally.nodes += (step - step0) - (tally.tris - tris0);
     W.i = i;
     W.step = step;
     W.best = best;
@@ -2153,12 +2177,12 @@ k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
     constexpr uint32_t WGT = heap_wg(HL), HT = heap_top_n(HL);
     const uint32_t lane = threadIdx.x & 63u;
-    // per-lane deferred-triangle list; with the culling BVH also the sphere walk's stack (never live together:
-    // the sphere scan finishes in the begin phase)
-    typedef typename std::conditional<(HL > 0), uint16_t, uint32_t>::type LT;
-    constexpr int SPHERE_STACK = HL > 0 ? 8 : (int)TRI_BATCH;
-    __shared__ uint32_t lane_words[(HL > 0 ? TRI_BATCH / 2 : TRI_BATCH) * WGT];
-    LT* const cand = (LT*)(lane_words + threadIdx.x);  // (list_at: a lane's entries stay in its own words)
+    // per-lane deferred-triangle list (leaf-pair entries); with the culling BVH also the sphere walk's stack (never
+    // live together: the sphere scan finishes in the begin phase)
+    constexpr uint32_t LIST_WORDS = HL > 0 ? TRI_BATCH / 2 : TRI_BATCH;
+    constexpr int SPHERE_STACK = (int)LIST_WORDS;
+    __shared__ uint32_t lane_words[LIST_WORDS * WGT];
+    uint32_t* const cand = lane_words + threadIdx.x;  // entry k at cand[k * WGT]: a lane's entries stay in its own words
     uint32_t* const sstack = lane_words + threadIdx.x;
     __shared__ float4 heap_top[HL > 0 ? 2 * HT : 1];
     if constexpr (HL > 0) {
@@ -2221,7 +2245,7 @@ k_trace_split_tris(const KParams P) {
         HRT_PHASE(1);
         HRT_LANES(1, have && qs == 3u);
         if (have && qs == 3u) {
-            if (heap_run<true, LT, HT, WGT>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
+            if (heap_run<true, HT, WGT, LIST_WORDS>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 4u);
