@@ -557,50 +557,9 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
 // node tests, and triangle tests run with most lanes active instead of one divergent branch per step.
 constexpr uint32_t TRI_BATCH = 16;  // measured on C4: 4 -> 5.89, 8 -> 6.28, 16 -> 6.38 Grays/s
 
-__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
-                                         uint32_t* cand) {
-    const f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    const uint32_t n = P.n, m = P.m;
-    uint32_t i = 1, nc = 0, step = 0;
-    bool walking = true;
-    while (true) {
-        // walk until this lane's walk ends or some lane's list is full (nc <= TRI_BATCH by construction:
-        // a lane appends at most once per step and every step re-checks the whole wave first)
-        while (walking && __ballot(nc == TRI_BATCH) == 0ull) {
-            bool advance = true;
-            if (i < n) {
-                tally.nodes++;
-                if (node_hit(P, i, r.o, inv)) {
-                    i *= 2u;
-                    advance = false;
-                }
-            } else {
-                const uint32_t j = i - n;
-                if (j >= m) {
-                    walking = false;
-                    advance = false;
-                } else {
-                    tally.tris++;
-                    cand[(nc++) * 256u] = j;
-                }
-            }
-            if (advance) {
-                i >>= __builtin_ctz(~i);  // while (i & 1) i /= 2
-                if (i == 0u) walking = false;
-                i++;
-            }
-            if (++step == 600u) walking = false;  // the reference's step cap
-        }
-        for (uint32_t k = 0; k < nc; k++) tri_test(P, r, cand[k * 256u], best, bj);  // in the order reached
-        nc = 0;
-        if (__ballot(walking) == 0ull) break;
-    }
-}
-
-// The same walk, split for k_trace_split_tris: heap_begin / heap_run (suspendable: returns false once
-// fewer than `below` lanes of the wave are still walking, after a flush, so no deferred triangle is
-// pending) with the walk state in HeapWalk. The walk, its step cap and the order of the triangle tests
-// are unchanged, so the winner and the node/triangle counts are those of walk_bvh.
+// The walk is split for k_trace_split_tris: heap_begin / heap_run (suspendable: returns false once fewer than
+// `below` lanes of the wave are still walking, after a flush, so no deferred triangle is pending) with the walk
+// state in HeapWalk; walk_bvh runs it to completion (k_trace, k_render).
 struct HeapWalk {
     f3 inv;           // 1 / d, the value intersect_node recomputes per node
     uint32_t i, step;
@@ -701,6 +660,15 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
     W.best = best;
     W.bj = bj;
     return walking == 0u;
+}
+
+__device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
+                                         uint32_t* cand) {
+    HeapWalk W;
+    heap_begin(r, best, W);
+    heap_run<false>(P, r, W, tally, cand, 0u);
+    best = W.best;
+    bj = W.bj;
 }
 
 // Opt-in triangle walk (rt_params.tri_bvh = 1; host/tri_bvh.hpp): an ordered, culling stack walk of a
