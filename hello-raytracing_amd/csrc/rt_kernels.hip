@@ -295,8 +295,9 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
     const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
     const float D = dl * 1.001f + (H16 ? P.bvh_rr_h : P.bvh_rr);
-    const float dn = __builtin_amdgcn_sqrtf(a);
-    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D + 4e-23f / dn;
+    // the last term bounds 4e-23 / |d| from above: v_rsq_f32 (1 ulp) times 1 + 2.5e-5 (no IEEE division per query)
+    const float delta = P.pad_k1 + fmin_ieee(P.pad_k2 * (D * D), P.pad_k3 * D) + P.pad_k4 * D +
+                        4.0001e-23f * __builtin_amdgcn_rsqf(a);
     const float pad = 2.02f * delta;
     Q.S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
     Q.S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);

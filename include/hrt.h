@@ -98,9 +98,9 @@ typedef struct rt_params {
                                   Tests: with few slots nearly every job waits for one                    */
     uint32_t fail_alloc_above_mb; /* fault injection for tests: colour-fold allocations above this many MiB
                                   fail as a refused hipMalloc would (0 = off); the draw then shrinks them */
-    uint32_t heap_lds;         /* triangle / mixed programs: 0 auto = the top eight levels of the implicit heap
-                                  in LDS with 16-bit triangle lists whenever m <= 65535 (k_trace_split_tris<..,
-                                  true>), 1 off (every node from L1/L2); bit-identical either way          */
+    uint32_t heap_lds;         /* triangle / mixed programs: 0 auto = nodes 1..991 of the implicit heap in LDS
+                                  (k_trace_split_tris<.., HL = 3>), 1 off (every node from L1/L2), 2 / 3 / 4 =
+                                  nodes 1..255 / 1..511 / 1..991; bit-identical always                      */
     uint32_t steal;            /* sample queue with the sample buffer, suspendable-walk kernels: frame-block work
                                   stealing (a wave whose job queue is drained claims single frames of other
                                   waves' jobs, so no long job trails the launch): 0 auto = on for launches of
@@ -161,7 +161,8 @@ int rt_set_camera(rt_renderer *r, const void *camera80);
  * renderer.rs:350-353 (group1 binding 0). n spheres of 48 B; slots past n are zero, like the wgpu buffer. */
 int rt_set_spheres(rt_renderer *r, const void *spheres48, uint32_t n);
 /* SceneTris::write_tree_data — scene_tris.rs:21-44 (group1 bindings 0..3): sizes = [n, m] (bvh_tree_size),
- * n Node (index 0 unused), m Triangle, k Material. */
+ * n Node (index 0 unused), m Triangle, k Material. n must be a power of two, as Tree::build makes it
+ * (tree.rs:38, m.next_power_of_two()); RT_ERR_ARG otherwise. */
 int rt_set_bvh(rt_renderer *r, const uint32_t sizes[2], const void *nodes32, uint32_t n_nodes,
                const void *tris64, uint32_t n_tris, const void *mats32, uint32_t n_mats);
 
