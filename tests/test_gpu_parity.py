@@ -799,6 +799,35 @@ def test_small_tris_scenes_vs_oracle(builder):
     assert_parity(scene.renderer.read_image(), ref, builder)
 
 
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 5, 8])
+def test_tiny_heaps_leaf_pairs_vs_oracle(k):
+    """Leaf-pair walk edge cases (DESIGN §4 Leaf pairs): k triangles give n = 1 (the root is leaf 0), 2, 4, 8,
+    with m odd / even / = n, so the walk's last leaf body falls inside or after a pair; both schedules (tiles:
+    walk_bvh, queue: the suspendable heap_run) against the oracle, with its node and triangle test counts."""
+    lines, faces = [], []
+    for t in range(k):  # a fan of overlapping triangles in front of the quad camera, at several depths
+        a = -1.2 + 0.3 * t
+        lines += [f"v {a:.3f} -0.8 {-0.2 * t:.3f}", f"v {a + 1.1:.3f} -0.6 {-0.1 * t:.3f}", f"v {a + 0.4:.3f} 0.9 0.0"]
+        faces.append(f"f {3 * t + 1} {3 * t + 2} {3 * t + 3}")
+    obj = ("\n".join(lines + faces) + "\n").encode()
+    tree = hrt.Tree.from_mesh(hrt.Mesh.load_obj(obj, hrt.Material.new_metal(hrt.Vec3(0.6, 0.5, 0.4), 0.3)))
+    tree.build()
+    sizes, nodes, tris, mats = tree.view()
+    assert sizes[1] == k and sizes[0] == max(1, 1 << (k - 1).bit_length()) if k else sizes == [1, 0]
+    camera = hrt.Camera.new(hrt.Vec3(0.0, 0.2, 3.5), hrt.Vec3(0.0, 0.1, -3.0), 2.2, 0.0, hrt.PI * hrt.f32(0.3))
+    sd = scenes.SceneDef(f"tiny{k}", hrt.RT_MODE_TRIS, 48, 32, camera, bvh=(sizes, nodes, tris, mats), frames=3)
+    ref, q = scenes.oracle_render(sd)
+    from oracle import oracle as O
+    want = (q, O.last_counts["node_tests"], O.last_counts["tri_tests"])
+    for schedule in (hrt.RT_SCHEDULE_TILES, hrt.RT_SCHEDULE_QUEUE):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=schedule, job_frames=1)
+        r.draw_frames(sd.frames, 1000, 10)
+        assert_parity(r.read_image(), ref, f"{k} triangles, schedule {schedule}")
+        st = r.stats()
+        assert (st.queries, st.node_tests, st.tri_tests) == want, (schedule, want)
+
+
 @pytest.mark.parametrize("schedule", [1, 2])
 @pytest.mark.parametrize("variant", [1, 3, 4])
 def test_mixed_mode_suzanne_ground_vs_oracle(variant, schedule):
