@@ -129,7 +129,9 @@ def pmc_view(pm):
     return {"file": pm.get("_file"), "valu_issue_busy": round(busy, 4), "active_lanes": round(lanes, 2),
             "valu_lane_util": round(busy * lanes / 64.0, 4),
             "wait_frac": round(pm.get("SQ_WAIT_ANY", 0.0) / max(pm.get("SQ_WAVE_CYCLES", 1.0), 1.0), 4),
-            "salu_insts": pm.get("SQ_INSTS_SALU"), "valu_insts": pm.get("SQ_INSTS_VALU")}
+            "salu_insts": pm.get("SQ_INSTS_SALU"), "valu_insts": pm.get("SQ_INSTS_VALU"),
+            "l2_hit_rate": (round(pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"]), 4)
+                            if pm.get("TCC_HIT_sum", 0.0) + pm.get("TCC_MISS_sum", 0.0) > 0 else None)}
 
 
 def launcher_selftest(args) -> int:
