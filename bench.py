@@ -148,7 +148,7 @@ def launcher_selftest(args) -> int:
     if world > 1:
         dist.init_process_group("gloo")
     H, W = 37, 5
-    block = row_block_for(args, H, world)
+    block = args.row_block
     rows = rank_rows(rank, world, H, block)
     part = torch.zeros((max_rows(world, H, block), W, 3), dtype=torch.float32)
     part[: len(rows)] = torch.from_numpy(rows.astype("float32"))[:, None, None]
@@ -191,13 +191,6 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
 MODE_NAMES = {0: "sphere", 1: "tris", 2: "mixed"}
 
 
-def row_block_for(args, height: int, world: int) -> int:
-    """--row-block, or (0 = auto) the balanced block of hrt.parallel.balanced_block for this height and rank count."""
-    from hrt.parallel import balanced_block
-
-    return args.row_block if args.row_block > 0 else balanced_block(height, world)
-
-
 def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_rays: float) -> dict:
     """Single-GPU proxy of the n-rank row split: every rank's share (rank_params(k, n, row_block)) rendered on
     this GPU in turn with the bench's step (reset, draw all frames, copy the image out, synchronise), warmed up
@@ -209,12 +202,11 @@ def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_r
 
     import scenes
     from hrt.parallel import assemble, rank_params
-    block = row_block_for(args, sd.height, n)
 
     shares, parts = [], []
     for k in range(n):
         rk = scenes.make_renderer(sd)
-        rk.set_params(**rank_params(k, n, block), **knobs)
+        rk.set_params(**rank_params(k, n, args.row_block), **knobs)
         buf = torch.zeros((rk.local_rows, sd.width, 3), dtype=torch.float32, device="cuda")
 
         def share_step():
@@ -243,11 +235,11 @@ def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_r
     slowest = max(s["ms_per_step"] for s in shares)
     same = None
     if full_img is not None:
-        whole = assemble(parts, sd.height, n, block=block)
+        whole = assemble(parts, sd.height, n, block=args.row_block)
         same = bool(torch.equal(whole.view(torch.int32), full_img.cpu().view(torch.int32)))
     return {
         "ranks": n,
-        "row_block": block,
+        "row_block": args.row_block,
         "full_ms_per_step": round(full_s * 1e3, 3),
         "full_mrays_s": round(full_rays / full_s / 1e6, 1),
         "predicted_ms_per_step": slowest,
@@ -296,10 +288,9 @@ def main() -> int:
     ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=128)
-    ap.add_argument("--row-block", type=int, default=0,
+    ap.add_argument("--row-block", type=int, default=8,
                     help="multi-GPU split: rows per block dealt round-robin (8 = whole 8x8 tile rows; 1 = single "
-                         "interleaved rows; 0 = auto: the largest power of two <= 8 that gives every rank the same "
-                         "number of rows, hrt.parallel.balanced_block)")
+                         "interleaved rows)")
     ap.add_argument("--emulate-ranks", type=int, default=None,
                     help="single-GPU proxy of the N-rank split: render every rank's share here in turn after the "
                          "timed region (default 8 on a one-rank run, 0 = off)")
@@ -365,10 +356,9 @@ def main() -> int:
         extra["tail_split"] = args.tail_split
     knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
                  tri_bvh=args.tri_bvh, **extra)
-    block = row_block_for(args, sd.height, world)
-    r.set_params(**rank_params(rank, world, block), **knobs)
+    r.set_params(**rank_params(rank, world, args.row_block), **knobs)
     local_rows = r.local_rows
-    part = torch.zeros((max_rows(world, sd.height, block), sd.width, 3), dtype=torch.float32, device=dev)
+    part = torch.zeros((max_rows(world, sd.height, args.row_block), sd.width, 3), dtype=torch.float32, device=dev)
     gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
     full = torch.empty((sd.height, sd.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
 
@@ -382,7 +372,7 @@ def main() -> int:
         r.draw_frames(sd.frames, 1000, 10)
         r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
         st = r.stats()
-        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=block)
+        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=args.row_block)
         if world > 1:
             # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
             # renderer's own stream, which does not order against it: finish the gather first
@@ -506,7 +496,7 @@ def main() -> int:
                 "rays_per_step": round(total_q / args.steps),
                 "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
                 "parallelism": f"rows{world}",
-                "row_block": block,
+                "row_block": args.row_block,
                 # how the sample queue folded the colours in frame order (rt_params.queue_budget_mb):
                 # "sample-buffer" (+ k_accumulate) or the bounded-memory "fold-ring"; device bytes it used
                 "fold": ("fold-ring" if st_last.fold_ring else "sample-buffer") if schedule == 2 else "in-register",

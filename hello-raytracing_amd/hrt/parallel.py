@@ -18,18 +18,6 @@ from __future__ import annotations
 import numpy as np
 
 
-def balanced_block(height: int, world: int, max_block: int = 8) -> int:
-    """The largest power-of-two block <= max_block that deals the image evenly: height a multiple of the block and
-    the block count a multiple of world, so every rank renders the same number of rows (C3 at 8 ranks: 1080 rows are
-    135 blocks of 8, 17 for seven ranks and 16 for one, but 1080 single rows are 135 each). 1 when none is."""
-    b = max(int(max_block), 1)
-    while b > 1:
-        if height % b == 0 and (height // b) % world == 0:
-            return b
-        b //= 2
-    return 1
-
-
 def rank_params(rank: int, world: int, block: int = 1) -> dict:
     """rt_params fields of rank `rank` of `world` (Renderer.set_params(**rank_params(...)))."""
     return {"row0": block * rank, "row_step": world, "row_block": block}
