@@ -400,9 +400,29 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #endif
             const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
             for (uint32_t j = 0; j < cnt; j++) {
-                const float t = exact_t_geo<SELECT>(P.bvh_sph[first + j], r, a4, a2);
+                float4 g;
+                if constexpr (SELECT) {  // (k_trace_split) buffer loads at 32-bit offsets: no 64-bit address kept and
+                                         // stepped per sphere (C3 +0.5 %; the mixed kernels have no SGPRs for the
+                                         // descriptors)
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+                    const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((first + j) * 16u), 0, 0);
+                    g = float4{v.x, v.y, v.z, v.w};
+                } else {
+                    g = P.bvh_sph[first + j];
+                }
+                const float t = exact_t_geo<SELECT>(g, r, a4, a2);
                 if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
-                    if (t < bt || (bc >= 0 && P.bvh_slot[first + j] < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
+                    int slot;
+                    if constexpr (SELECT) {
+                        const __amdgpu_buffer_rsrc_t rsl =
+                            __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+                        slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)((first + j) * 4u), 0, 0);
+                    } else {
+                        slot = P.bvh_slot[first + j];
+                    }
+                    if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                 }
             }
             tally.spheres += cnt;
