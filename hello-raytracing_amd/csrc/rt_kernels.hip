@@ -562,8 +562,22 @@ __device__ __forceinline__ void tri_record(const KParams& P, const Ray& r, const
 
 // The reference's per-leaf update: accept t in [1e-4, best). The walks only track (best, bj); the hit
 // record is built once for the winner (closest_hit), which keeps fewer registers live during the walk.
+template <bool TBUF = false>
 __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_t j, float& best, int& bj) {
-    const float t = tri_t(r, P.tris[j]);
+    TriDev tr;
+    if constexpr (TBUF) {  // a, e1, e2 through buffer loads at 32-bit offsets (no 64-bit address per triangle)
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.tris, (short)0, (int)(P.m * 64u), 0x00020000);
+        const f4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j * 64u), 0, 0);
+        const f4v e1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j * 64u + 16u), 0, 0);
+        const f4v e2 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j * 64u + 32u), 0, 0);
+        tr.a = float4{a.x, a.y, a.z, a.w};
+        tr.e1 = float4{e1.x, e1.y, e1.z, e1.w};
+        tr.e2 = float4{e2.x, e2.y, e2.z, e2.w};
+    } else {
+        tr = P.tris[j];
+    }
+    const float t = tri_t(r, tr);
     if (t >= 1e-4f && t < best) {
         best = t;
         bj = (int)j;
@@ -614,7 +628,7 @@ constexpr uint32_t PAIR_BIT = 0x80000000u;
 // triangles.)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;  // 32-bit LDS addressing for the list
 
-template <bool SUSPEND, uint32_t HT = 0, uint32_t LS = 256, uint32_t CAP = TRI_BATCH>
+template <bool SUSPEND, uint32_t HT = 0, uint32_t LS = 256, uint32_t CAP = TRI_BATCH, bool TBUF = false>
 __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand_g,
                                          uint32_t below, const float4* __restrict__ top = nullptr) {
     // the list's LDS byte address (32-bit arithmetic): entry k at c0 + k * 4 LS
@@ -666,8 +680,8 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
         for (uint32_t k = 0; k < nc; k++) {  // in the order reached
             const uint32_t e = *(const lds_u32*)(uintptr_t)(c0 + __umul24(k, 4u * LS));
             const uint32_t j = e & ~PAIR_BIT;
-            tri_test(P, r, j, best, bj);
-            if (e & PAIR_BIT) tri_test(P, r, j + 1u, best, bj);
+            tri_test<TBUF>(P, r, j, best, bj);
+            if (e & PAIR_BIT) tri_test<TBUF>(P, r, j + 1u, best, bj);
         }
         nc = 0u;
         if (walking == 0u) break;
@@ -1098,7 +1112,8 @@ __device__ __forceinline__ uint32_t sample_ref(const WaveJobs& J, uint32_t f0, u
 __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint32_t ref, const f3 c) {
     const KPtr K = kargs();
     if (!K->ring_mode) {  // sample buffer: the colour at its frame of the launch, folded by k_accumulate
-        float* o = K->samples + ((size_t)ref * K->tiles_w * K->tiles_h * 64u + pix) * 3u;
+        const uint32_t npix = K->tiles_w * K->tiles_h * 64u;  // tile-padded pixels of a frame (< 2^32)
+        float* o = K->samples + ((unsigned long long)ref * npix + pix) * 3u;  // one 32 x 32 + 64 multiply-add
         o[0] = c.x;
         o[1] = c.y;
         o[2] = c.z;
@@ -2234,7 +2249,8 @@ k_trace_split_tris(const KParams P) {
         HRT_PHASE(1);
         HRT_LANES(1, have && qs == 3u);
         if (have && qs == 3u) {
-            if (heap_run<true, HT, WGT, LIST_WORDS>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
+            // (TBUF: the culling-BVH mixed kernel has no SGPRs for the triangle buffer descriptor)
+            if (heap_run<true, HT, WGT, LIST_WORDS, SCAN != SCAN_BVH>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 4u);
