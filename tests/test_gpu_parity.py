@@ -932,6 +932,10 @@ def test_bad_arguments_fail_loudly():
     with pytest.raises(hrt.RtError):  # sizes larger than the node buffer
         r.write_bvh([4, 1], np.zeros(2, dtype=hrt.NODE_DTYPE), np.zeros(1, dtype=hrt.TRIANGLE_DTYPE),
                     np.zeros(1, dtype=hrt.MATERIAL_DTYPE))
+    for n in (0, 3, 6):  # Tree::build makes n a power of two (the leaf-pair walk relies on it)
+        with pytest.raises(hrt.RtError):
+            r.write_bvh([n, 1], np.zeros(8, dtype=hrt.NODE_DTYPE), np.zeros(1, dtype=hrt.TRIANGLE_DTYPE),
+                        np.zeros(1, dtype=hrt.MATERIAL_DTYPE))
     small = np.zeros(10, dtype=np.float32)
     assert hrt.lib().rt_read_image(r._h, small.ctypes.data_as(hrt._lib._PF), small.size) == hrt._lib.RT_ERR_ARG
     for bad in ({"variant": 2}, {"variant": 9}, {"schedule": 3}, {"tri_bvh": 2}, {"row_step": 0},
