@@ -461,12 +461,12 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
-template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256>
+template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256, bool KA = false>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin<H16>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16, LS>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
-    return bvh_end(P, r, Q, best, tally);
+    if (bvh_begin<H16, false, KA>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16, LS>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
+    return bvh_end<KA>(P, r, Q, best, tally);
 }
 
 // (p - c) / radius, exact: the host's correctly rounded 1 / radius and two residual corrections
@@ -2238,7 +2238,7 @@ k_trace_split_tris(const KParams P) {
                 qs = 3u;
             } else {
                 float sb = FLT_MAX_REF;
-                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT>(P, ray, sb, sstack, tally);
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
@@ -2249,8 +2249,9 @@ k_trace_split_tris(const KParams P) {
         HRT_PHASE(1);
         HRT_LANES(1, have && qs == 3u);
         if (have && qs == 3u) {
-            // (TBUF: the culling-BVH mixed kernel has no SGPRs for the triangle buffer descriptor)
-            if (heap_run<true, HT, WGT, LIST_WORDS, SCAN != SCAN_BVH>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
+            // (triangles through a buffer descriptor: C4 +0.7 %; the culling-BVH mixed kernel makes room for it by reading
+            // its sphere walk's rare-path constants through kargs(): C5 +1.2 %)
+            if (heap_run<true, HT, WGT, LIST_WORDS, true>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 4u);
