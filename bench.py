@@ -141,27 +141,77 @@ def launcher_selftest(args) -> int:
     import torch
     import torch.distributed as dist
 
-    from hrt.parallel import gather_image, max_rows, rank_rows
+    from hrt.parallel import gather_image, image_checksum, max_rows, rank_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+    # 37 rows: with 8-row blocks rank 4 of 5+ would own none; the rows carry their index and the column
     H, W = 37, 5
     block = args.row_block
     rows = rank_rows(rank, world, H, block)
     part = torch.zeros((max_rows(world, H, block), W, 3), dtype=torch.float32)
-    part[: len(rows)] = torch.from_numpy(rows.astype("float32"))[:, None, None]
+    part[: len(rows)] = (torch.from_numpy(rows.astype("float32"))[:, None, None] * 16.0
+                         + torch.arange(W, dtype=torch.float32)[None, :, None])
+    t0 = time.perf_counter()
     full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0, block=block)
+    gather_s = time.perf_counter() - t0
+    local = {"rows": len(rows), "elapsed_s": 0.0, "trace_ms": 0.0, "gather_ms": gather_s * 1e3, "queries": 0,
+             "checksum": image_checksum(part, rows, W)}
+    report = rank_reports(local, world, dist if world > 1 else None, "cpu")
     if rank == 0:
-        ok = bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32)))
-        print(json.dumps({"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}",
-                          "row_block": block,
-                          "verify_gather_bitwise": ok}), flush=True)
+        ok = bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32) * 16.0))
+        out = {"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}", "row_block": block,
+               "verify_gather_bitwise": ok}
+        out.update(multi_rank_fields(report, image_checksum(full, range(H), W), 1))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def rank_reports(local: dict, world: int, dist, device) -> list:
+    """Every rank's own figures (rows owned, timed-region wall time, trace kernel time, gather time, rays, image
+    checksum), collected on every rank by one all_gather after the timed region (the 8-GPU run is the
+    driver's alone, so its line must say what each rank did)."""
+    import torch
+
+    keys = ("rows", "elapsed_s", "trace_ms", "gather_ms", "queries")
+    t = torch.tensor([float(local[k]) for k in keys], dtype=torch.float64, device=device)
+    # (the checksum as a signed 64-bit word)
+    c = torch.tensor([((int(local["checksum"]) + 2**63) % 2**64) - 2**63], dtype=torch.int64, device=device)
+    if dist is None:
+        ts, cs = [t], [c]
+    else:
+        ts = [torch.zeros_like(t) for _ in range(world)]
+        cs = [torch.zeros_like(c) for _ in range(world)]
+        dist.all_gather(ts, t)
+        dist.all_gather(cs, c)
+    out = []
+    for k in range(world):
+        v = ts[k].cpu().tolist()
+        d = {"rank": k, **{key: v[i] for i, key in enumerate(keys)}, "checksum": int(cs[k].cpu().item())}
+        d["rows"], d["queries"] = int(d["rows"]), int(d["queries"])
+        out.append(d)
+    return out
+
+
+def multi_rank_fields(report: list, full_checksum: int, steps: int) -> dict:
+    """The JSON line's per-rank block: per-rank elapsed / trace / gather times and rows, the gather's own time, and
+    the destination rank's check that the gathered image's position-dependent checksum equals the sum of the ranks'
+    local ones (hrt.parallel.image_checksum; mod 2^64)."""
+    ranks = [{"rank": d["rank"], "rows": d["rows"], "elapsed_s": round(d["elapsed_s"], 4),
+              "trace_ms_per_step": round(d["trace_ms"] / steps, 3), "gather_ms_per_step": round(d["gather_ms"] / steps, 3),
+              "rays_per_step": round(d["queries"] / steps)} for d in report]
+    total = sum(d["checksum"] for d in report)
+    return {
+        "ranks": ranks,
+        "gather_ms_per_step": round(max(d["gather_ms"] for d in report) / steps, 3),
+        "slowest_rank": max(report, key=lambda d: d["elapsed_s"])["rank"],
+        "gather_checksum_ok": (total - int(full_checksum)) % 2**64 == 0,
+    }
 
 
 def cpu_baseline(sd, threads: int, rows: int, frames: int):
@@ -312,7 +362,7 @@ def main() -> int:
 
     import hrt  # noqa: F401  (loads lib/libhrt.so)
     import scenes
-    from hrt.parallel import gather_image, max_rows, rank_params
+    from hrt.parallel import gather_image, image_checksum, max_rows, owned_rows, rank_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -367,16 +417,23 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
+    gather_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    gather_ms = [0.0]
+
     def step():
         r.reset_frame_count()
         r.draw_frames(sd.frames, 1000, 10)
         r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
         st = r.stats()
+        gather_ev[0].record()
         gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=args.row_block)
+        gather_ev[1].record()
         if world > 1:
             # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
             # renderer's own stream, which does not order against it: finish the gather first
             torch.cuda.current_stream().synchronize()
+        gather_ev[1].synchronize()
+        gather_ms[0] += gather_ev[0].elapsed_time(gather_ev[1])
         return st
 
     log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
@@ -388,6 +445,7 @@ def main() -> int:
         log(f"warmup {i}: {time.perf_counter() - t:.2f} s")
 
     barrier()
+    gather_ms[0] = 0.0
     t0 = time.perf_counter()
     queries = 0
     kernel_ms = 0.0
@@ -438,6 +496,15 @@ def main() -> int:
         all_t = stats_t.cpu().numpy()[None]
     t_max = float(all_t[:, 0].max())
     total_q = float(all_t[:, 1].sum())
+    # per-rank figures and the gather's checksum check (multi-rank runs)
+    report = None
+    if world > 1:
+        local = {"rows": local_rows, "elapsed_s": elapsed, "trace_ms": trace_ms, "gather_ms": gather_ms[0],
+                 "queries": queries,
+                 "checksum": image_checksum(part, owned_rows(*[rank_params(rank, world, args.row_block)[k]
+                                                               for k in ("row0", "row_step")], sd.height,
+                                                             args.row_block), sd.width)}
+        report = rank_reports(local, world, dist, dev if args.backend == "nccl" else "cpu")
 
     if rank == 0:
         value = total_q / t_max / 1e6
@@ -539,6 +606,8 @@ def main() -> int:
                 "pmc": pmc_view(pmc),
             },
         }
+        if report is not None:
+            out.update(multi_rank_fields(report, image_checksum(full, range(sd.height), sd.width), args.steps))
         if emulated is not None:
             out["emulated_split"] = emulated
         if not args.no_cpu_baseline and world == 1:

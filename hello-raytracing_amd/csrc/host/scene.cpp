@@ -121,10 +121,9 @@ void stable_sort_pairs(std::vector<std::pair<float, uint32_t>>& v, std::vector<s
     for (size_t k = 0; k < len; k++) v[k].second = a[k].second;  // keys are not needed after the sort
 }
 
-unsigned default_threads() {
-    if (const char* e = std::getenv("HRT_HOST_THREADS")) return (unsigned)std::max(1, std::atoi(e));
-    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-}
+// (the library reads no environment variables: a caller that wants another count passes it to
+// rt_host_tree_build_threads)
+unsigned default_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
 
 }  // namespace
 

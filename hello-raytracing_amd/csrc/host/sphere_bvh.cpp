@@ -173,13 +173,7 @@ SphereBvh build_sphere_bvh(const std::vector<float>& cr) {
     }
     Builder b;
     b.out = &out;
-#ifdef HRT_BVH_TUNING  // tree-shape sweeps only (make EXTRA=-DHRT_BVH_TUNING); the product reads no environment
-    if (const char* e = std::getenv("HRT_BVH_MAX_LEAF")) b.max_leaf = std::max(1, std::min(15, std::atoi(e)));
-    if (const char* e = std::getenv("HRT_BVH_LEAF_DEPTH")) b.leaf_depth = (uint32_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("HRT_BVH_TRAVERSAL_COST")) b.traversal_cost = std::atof(e);
-    if (const char* e = std::getenv("HRT_BVH_ALL_AXES")) b.all_axes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("HRT_BVH_BINS")) b.bins = std::max(2, std::min(64, std::atoi(e)));
-#endif
+    // (the tree-shape parameters are fixed: Builder's defaults, chosen by the round-2 sweeps in DESIGN.md §4)
     bool any = false;
     for (size_t i = 0; i < n; i++) {
         const float* s = &cr[4 * i];

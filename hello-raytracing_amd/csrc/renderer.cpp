@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/hrt.h"
+#include "../../include/hrt_testing.h"
 #include "host/scene.hpp"
 #include "host/sphere_bvh.hpp"
 #include "host/tri_bvh.hpp"
@@ -60,7 +61,7 @@ struct DevBuf {
     }
 };
 
-// fail_above: fault injection for tests (rt_params.fail_alloc_above_mb), an allocation above that many bytes
+// fail_above: fault injection for tests (rt_testing_set_faults), an allocation above that many bytes
 // fails as a refused hipMalloc would (0 = off)
 template <typename T>
 int ensure(DevBuf<T>& b, size_t n, size_t fail_above = 0) {
@@ -68,7 +69,7 @@ int ensure(DevBuf<T>& b, size_t n, size_t fail_above = 0) {
     b.release();
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
     if (fail_above && bytes > fail_above)
-        return fail(RT_ERR_ALLOC, "hipMalloc: injected failure (rt_params.fail_alloc_above_mb)");
+        return fail(RT_ERR_ALLOC, "hipMalloc: injected failure (rt_testing_set_faults)");
     hipError_t e = hipMalloc((void**)&b.ptr, bytes);
     if (e != hipSuccess) {
         b.ptr = nullptr;
@@ -148,6 +149,10 @@ struct rt_renderer {
     uint32_t time = 0, frame_count = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // pipelined band launches of the sample buffer (launch_frames): band i traces on side[i % 2], its k_accumulate
+    // runs on `stream`; fork / trace-done / accumulate-done events (no timing)
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_tdone[2] = {nullptr, nullptr}, ev_adone[2] = {nullptr, nullptr};
 
     DevBuf<float> image;
     DevBuf<float4> sph_geo;
@@ -173,6 +178,7 @@ struct rt_renderer {
     DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
     uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
+    DevBuf<float> samples2;     // the second band buffer of the pipelined band launches (launch_frames)
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
@@ -189,7 +195,9 @@ struct rt_renderer {
     uint32_t trace_pairs = 0, trace_pairs_pending = 0;
     uint32_t last_schedule = 0;
     uint32_t last_suspend = 0;
+    uint32_t test_ring_slots_max = 0, test_fail_alloc_above_mb = 0;  // hrt_testing.h fault injection
     uint32_t ring_slots = 0;  // fold-ring slots of the last sample-queue draw
+    uint32_t stats_bands = 0; // row bands of the last sample-queue draw's launches (1: one launch covers every row)
     uint32_t ring_tiles = 0, ring_nchunks = 0;  // (diagnostics: HRT_RING_DUMP)
     size_t ring_ctl_words = 0;
     uint64_t fold_bytes = 0;  // device memory of the last sample-queue draw's colour fold (rt_stats.fold_bytes)
@@ -199,7 +207,7 @@ struct rt_renderer {
     uint64_t device_bytes() const {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
-               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + samples2.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
@@ -520,7 +528,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 
     uint32_t launches = 0;
     hrt_reset_last_kernel();  // (a draw that launches nothing reports no kernel)
-    if (schedule == RT_SCHEDULE_QUEUE) {
+    if (P.nrows == 0u) {  // a renderer that owns no rows (row0 at or below the last row): nothing to trace
+        r->trace_pairs = 0;
+        HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+    } else if (schedule == RT_SCHEDULE_QUEUE) {
         r->trace_pairs_pending = 0;
         P.tiles_w = (r->width + 7u) / 8u;
         P.tiles_h = (P.nrows + 7u) / 8u;
@@ -534,7 +545,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.tri_small = 0u;
         if (r->mode != RT_MODE_SPHERE &&
             (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
-            P.tri_small = r->params.heap_lds >= 2u ? r->params.heap_lds - 1u : HRT_HEAP_AUTO;
+            P.tri_small = HRT_HEAP_AUTO;
         if (variant == hrt_dev::SCAN_DEFER && r->mode == RT_MODE_MIXED && P.tri_small > 1u) P.tri_small = 1u;
         // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for k_trace's
         // cheap sphere scans (C2: 32 costs 3 %); a power of two (the ring's slot layout)
@@ -542,36 +553,67 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.jf_log2 = 0;
         while ((2u << P.jf_log2) <= std::min(jf, 1024u)) P.jf_log2++;
         jf = 1u << P.jf_log2;
-        // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a launch, then
-        // k_accumulate) when the budget holds at least min(count, 320) frames of colours, in launches of as many
-        // frames as it holds; else the fold ring in the budget (bounded memory: DESIGN.md §4). Shorter buffer
-        // launches lose to the ring (fewer jobs per tile spread the waves over more of the image: C3 at 82 /
-        // 164 / 344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1, the 1 GiB ring 30.2 / 8.1).
+        // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a
+        // launch, then k_accumulate) or the bounded-memory fold ring. With the sample buffer a launch covers
+        //   1. the whole draw (every row, every frame) when its colours fit the budget: one buffer;
+        //   2. else, when one tile row x every frame fits half the budget, a BAND of tile rows x every frame: the
+        //      bands run as pipelined launches on two side streams with two buffers — band i + 1's trace fills the
+        //      CUs band i's drain leaves idle, band i's k_accumulate (on the renderer stream) runs beside it, and band
+        //      i + 2 reuses band i's buffer once that fold is done — so the colour memory is bounded by the budget while
+        //      every tile still has all its frames (and jobs) in one launch, the coherence a launch of fewer frames
+        //      loses (C3 at 82 / 164 / 344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1);
+        //   3. else frame chunks of the whole image, as many frames as the budget holds; the fold ring (auto) when that
+        //      is under min(count, 320) frames.
         size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
-        const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
-        P.ring_mode = budget / (frame_floats * 4u) < std::min<uint32_t>(std::max(count, 1u), 320u) ? 1u : 0u;
+        const size_t row_floats = (size_t)P.tiles_w * 64u * 3u;      // one tile row x one frame (tile-padded)
+        const size_t frame_floats = row_floats * P.tiles_h;
+        const size_t fail_above = (size_t)r->test_fail_alloc_above_mb << 20;
+        uint32_t chunk = std::max(count, 1u), bt = P.tiles_h, log2s = 0;
+        bool bands = false;
+        // (a band launch needs jobs for the persistent grid: at least 64 per CU — 16 Ki on MI355X, 2.3 per resident wave
+        // of k_trace_split; a band of half an 8 GiB budget holds 174 Ki 32-frame jobs whatever the frame count)
+        const uint64_t band_jobs_min = 64ull * std::max(r->cus, 1u);
+        const uint32_t bt_fit = (uint32_t)std::min<size_t>(P.tiles_h, (budget / 2u) / (row_floats * 4u * chunk));
+        if (r->params.fold != RT_FOLD_RING && frame_floats * 4u * chunk > budget && bt_fit >= 1u &&
+            (uint64_t)bt_fit * P.tiles_w * ((chunk + jf - 1u) / jf) >= band_jobs_min) {
+            bands = true;
+            const uint32_t nb = (P.tiles_h + bt_fit - 1u) / bt_fit;
+            bt = (P.tiles_h + nb - 1u) / nb;  // balanced bands
+        } else if (frame_floats * 4u * chunk > budget) {
+            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+        }
+        P.ring_mode = !bands && chunk < std::min<uint32_t>(std::max(count, 1u), 320u) ? 1u : 0u;
         if (r->params.fold == RT_FOLD_BUFFER) P.ring_mode = 0u;  // forced (measurements, tests)
         if (r->params.fold == RT_FOLD_RING) P.ring_mode = 1u;
-        const size_t fail_above = (size_t)r->params.fail_alloc_above_mb << 20;
-        uint32_t chunk = 1, log2s = 0;
         size_t zero_words = 0;
         if (!P.ring_mode) {
             r->ring.release();  // the other fold's memory: the draw's colour memory stays within the budget
             r->ring_ctl.release();
-            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
-            // a device short of memory gets smaller launches, down to one frame, instead of a failed draw
-            const size_t buf_budget = std::max(budget, frame_floats * 4u);
-            while ((rc = ensure_within(r->samples, (size_t)chunk * frame_floats, buf_budget, fail_above)) == RT_ERR_ALLOC &&
-                   chunk > 1u) {
+            // a device short of memory gets thinner bands, then fewer frames per launch, down to one frame, instead
+            // of a failed draw
+            for (;;) {
+                const size_t need = (size_t)bt * chunk * row_floats;
+                const size_t cap = std::max(bands ? budget / 2u : budget, need * 4u);
+                rc = ensure_within(r->samples, need, cap, fail_above);
+                if (!rc && bands) rc = ensure_within(r->samples2, need, cap, fail_above);
+                if (rc != RT_ERR_ALLOC) break;
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
-                chunk = (chunk + 1u) / 2u;
+                r->samples2.release();
+                if (bands && bt > 1u) {
+                    bt = (bt + 1u) / 2u;
+                } else if (chunk > 1u) {
+                    chunk = (chunk + 1u) / 2u;
+                } else {
+                    break;
+                }
             }
             if (rc) return rc;
-            P.samples = r->samples.ptr;
+            if (!bands) r->samples2.release();
             r->ring_slots = 0;
-            r->fold_bytes = (uint64_t)chunk * frame_floats * 4u;
+            r->fold_bytes = (uint64_t)(bands ? 2u : 1u) * bt * chunk * row_floats * 4u;
         } else {
             r->samples.release();
+            r->samples2.release();
             // frames per launch: at most FOLD_MAX_JOBS jobs per tile (the done bits of the tile's fold word)
             chunk = std::max(1u, std::min(count, hrt_dev::FOLD_MAX_JOBS * jf));
             const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
@@ -583,8 +625,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 const size_t fit = std::max<size_t>(1, budget / ((size_t)jf << 10));
                 log2s = 0;
                 while ((2ull << log2s) <= fit && (1ull << log2s) < jobs && log2s < 20u) log2s++;
-                // rt_params.ring_slots_max caps the slots (tests: jobs then wait in the free queue for a slot)
-                while (r->params.ring_slots_max && log2s > 0 && (1ull << log2s) > r->params.ring_slots_max) log2s--;
+                // rt_testing_set_faults caps the slots (tests: jobs then wait in the free queue for a slot)
+                while (r->test_ring_slots_max && log2s > 0 && (1ull << log2s) > r->test_ring_slots_max) log2s--;
                 zero_words = 2ull * ntiles + (4ull << log2s) + 4u;
                 const size_t ring_floats4 = ((size_t)jf << log2s) * 64u;
                 rc = ensure_within(r->ring, ring_floats4, std::max(budget, ring_floats4 * 16u), fail_above);
@@ -610,60 +652,90 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             r->fold_bytes = (uint64_t)P.ring_bytes + 4ull * (4u * r->ring_slots + 4u) + 4ull * r->ring_ctl_words -
                             4ull * zero_words + 8ull * ntiles;
         }
-        P.queue = r->counter.ptr + 15;
         // frame-block work stealing (rt_kernels.hip steal_block): the suspendable-walk kernels with the sample
-        // buffer; one slot per resident wave, at most 32 waves per CU
-        // Auto: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job dealt
-        // late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for long
-        // launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 -> 0.88).
-        {
-            const uint64_t chunks0 = (std::min(chunk, count) + jf - 1u) / jf;
-            const uint64_t jobs0 = (uint64_t)ntiles * chunks0;
-            const bool fits = ntiles < (1u << 25) - 1u && chunks0 < 2048u;  // the slot's tile and chunk fields
-            const bool want = r->params.steal == 2u || (r->params.steal == 0u && jobs0 < 16ull * 24u * std::max(r->cus, 1u));
-            P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
-        }
+        // buffer; one slot per resident wave, at most 32 waves per CU (a half of the slots per side stream)
         P.steal_cap = 32u * std::max(r->cus, 1u);
-        rc = ensure(r->steal_slots, P.steal_cap);
+        rc = ensure(r->steal_slots, 2u * (size_t)P.steal_cap);
         if (rc) return rc;
-        P.steal_slots = r->steal_slots.ptr;
+        const uint32_t nrows_all = P.nrows, th_all = P.tiles_h;
+        float* const image0 = P.image;
+        const uint32_t nbands = bands ? (th_all + bt - 1u) / bt : 1u;
+        // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
+        P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
+        r->last_suspend = split ? r->params.suspend_below : 0u;
+        P.job_frames = jf;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+        if (bands) {  // the side streams start after everything already on the renderer stream (zeroed counters)
+            HIP_TRY(hipEventRecord(r->ev_fork, r->stream));
+            for (hipStream_t sst : r->side) HIP_TRY(hipStreamWaitEvent(sst, r->ev_fork, 0));
+        }
+        uint32_t li = 0;  // launch index
         for (uint32_t done = 0; done < count; done += chunk) {
-            P.nframes = std::min(chunk, count - done);
-            P.time0 = time0 + done * dtime;
-            P.frame0 = r->frame_count + done;
-            P.job_frames = jf;
-            P.suspend_below = split ? r->params.suspend_below : 0u;
-            r->last_suspend = P.suspend_below;
-            P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
-            P.njobs = (unsigned long long)ntiles * P.nchunks;
-            // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
-            // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
-            // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
-            P.tail_from = 0xFFFFFFFFu;
-            const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
-            if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
-                r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
-                const unsigned long long k = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
-                P.tail_from = (uint32_t)(P.njobs - k);
-                P.njobs += 3ull * k;
-            }
-            r->ring_nchunks = P.nchunks;
-            HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
-            if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
-            if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
-            rc = trace_events(r, r->trace_pairs_pending);
-            if (rc) return rc;
-            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
-            HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
-            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
-            r->trace_pairs_pending++;
-            launches++;
-            if (!P.ring_mode) {
-                HIP_TRY(hrt_launch_accumulate(P, r->stream));
+            for (uint32_t band = 0; band < nbands; band++, li++) {
+                const uint32_t k = bands ? (li & 1u) : 0u;  // side stream and buffer of this launch
+                P.kr0 = band * bt * 8u;
+                P.nrows = bands ? std::min(bt * 8u, nrows_all - P.kr0) : nrows_all;
+                P.tiles_h = bands ? (P.nrows + 7u) / 8u : th_all;
+                P.image = image0 + (size_t)P.kr0 * r->width * 3u;
+                P.samples = P.ring_mode ? nullptr : (k ? r->samples2.ptr : r->samples.ptr);
+                P.queue = r->counter.ptr + (k ? hrt_dev::QUEUE2 : 15u);
+                P.steal_slots = r->steal_slots.ptr + (size_t)k * P.steal_cap;
+                P.nframes = std::min(chunk, count - done);
+                P.time0 = time0 + done * dtime;
+                P.frame0 = r->frame_count + done;
+                P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
+                const uint32_t lt = P.tiles_w * P.tiles_h;  // tiles of this launch
+                P.njobs = (unsigned long long)lt * P.nchunks;
+                // Auto stealing: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job
+                // dealt late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for
+                // long launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 ->
+                // 0.88)
+                {
+                    const bool fits = lt < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
+                    const bool want = r->params.steal == 2u ||
+                                      (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
+                    P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
+                }
+                // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
+                // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
+                // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
+                P.tail_from = 0xFFFFFFFFu;
+                const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
+                if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
+                    r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
+                    const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
+                    P.tail_from = (uint32_t)(P.njobs - q);
+                    P.njobs += 3ull * q;
+                }
+                r->ring_nchunks = P.nchunks;
+                hipStream_t st = bands ? r->side[k] : r->stream;
+                if (bands && li >= 2u) HIP_TRY(hipStreamWaitEvent(st, r->ev_adone[k], 0));  // buffer k folded
+                HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), st));
+                if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), st));
+                if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), st));
+                rc = trace_events(r, r->trace_pairs_pending);
+                if (rc) return rc;
+                HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], st));
+                HIP_TRY(hrt_launch_trace(r->mode, variant, P, st));
+                HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], st));
+                r->trace_pairs_pending++;
                 launches++;
+                if (bands) {
+                    HIP_TRY(hipEventRecord(r->ev_tdone[k], st));
+                    HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_tdone[k], 0));
+                }
+                if (!P.ring_mode) {
+                    HIP_TRY(hrt_launch_accumulate(P, r->stream));
+                    launches++;
+                    if (bands) HIP_TRY(hipEventRecord(r->ev_adone[k], r->stream));
+                }
             }
         }
+        P.kr0 = 0u;
+        P.nrows = nrows_all;
+        P.tiles_h = th_all;
+        P.image = image0;
+        r->stats_bands = nbands;
         r->trace_pairs = r->trace_pairs_pending;
         r->trace_pairs_pending = 0;
     } else {
@@ -685,9 +757,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.launches = launches;
     r->stats.local_rows = P.nrows;
     std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
-    if (schedule == RT_SCHEDULE_QUEUE && count) {
+    if (schedule == RT_SCHEDULE_QUEUE && count && P.nrows) {
         r->stats.fold_ring = P.ring_mode;
         r->stats.fold_bytes = r->fold_bytes;
+        r->stats.bands = r->stats_bands;
     }
     r->stats.device_bytes = r->device_bytes();
     r->timing_pending = true;
@@ -771,6 +844,7 @@ void delete_buffers(rt_renderer* r) {
     r->counter.release();
     r->steal_slots.release();
     r->samples.release();
+    r->samples2.release();
     r->ring.release();
     r->ring_ctl.release();
     r->wave_trace.release();
@@ -822,8 +896,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.row_block = 1;
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
-    // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one chunk (one k_trace launch per draw, one launch
-    // tail instead of six): C3 25.9 -> 26.1 Grays/s over 4 GiB
+    // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one launch (pipelined bands: launch_frames)
     r->params.queue_budget_mb = 32768;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
@@ -832,8 +905,14 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     //           kernel); with the frame-block refill and 16-frame jobs 16 -> 25.2, 24 -> 25.9, 32 -> 25.2;
     //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92
     r->params.suspend_below = mode == RT_MODE_SPHERE ? 24u : 32u;
-    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_stop) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreate(&r->ev_start) == hipSuccess && hipEventCreate(&r->ev_stop) == hipSuccess &&
+              hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ok; k++)
+        ok = hipStreamCreateWithFlags(&r->side[k], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&r->ev_tdone[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&r->ev_adone[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         rt_destroy(r);
         return fail(RT_ERR_DEVICE, "rt_create: stream/event creation failed");
     }
@@ -850,10 +929,18 @@ int rt_destroy(rt_renderer* r) {
     if (!r) return RT_OK;
     DeviceScope ds(r->device);  // (frees on the renderer's device even if switching failed)
     if (r->stream) (void)hipStreamSynchronize(r->stream);
+    for (hipStream_t s : r->side)
+        if (s) (void)hipStreamSynchronize(s);
     delete_buffers(r);
     for (hipEvent_t e : r->ev_trace) (void)hipEventDestroy(e);
     if (r->ev_start) (void)hipEventDestroy(r->ev_start);
     if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
+    if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
+    for (int k = 0; k < 2; k++) {
+        if (r->ev_tdone[k]) (void)hipEventDestroy(r->ev_tdone[k]);
+        if (r->ev_adone[k]) (void)hipEventDestroy(r->ev_adone[k]);
+        if (r->side[k]) (void)hipStreamDestroy(r->side[k]);
+    }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;
@@ -869,7 +956,9 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (!r || !p) return fail(RT_ERR_ARG, "rt_set_params: null");
     DeviceScope ds(r->device);
     if (ds.rc) return ds.rc;
-    if (p->row_step == 0 || p->row0 >= r->height) return fail(RT_ERR_ARG, "rt_set_params: bad row partition");
+    // (row0 >= height: the renderer owns no rows, e.g. a rank beyond the image's last row block; its draws
+    // render nothing and its image is empty)
+    if (p->row_step == 0) return fail(RT_ERR_ARG, "rt_set_params: bad row partition (row_step 0)");
     if ((uint64_t)p->row_step * std::max(p->row_block, 1u) > (1ull << 30))
         return fail(RT_ERR_ARG, "rt_set_params: row_step x row_block too large");
     if (p->variant != 0 && p->variant != 1 && p->variant != 3 && p->variant != 4)
@@ -878,7 +967,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     if (p->suspend_below > 64) return fail(RT_ERR_ARG, "rt_set_params: suspend_below must be 0..64");
     if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
-    if (p->heap_lds > 4) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2-4");
+    if (p->heap_lds > 2) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2 on");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 1) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto or 1 off");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
@@ -918,14 +1007,8 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     DeviceScope ds(r->device);
     if (ds.rc) return ds.rc;
     const uint32_t n = sizes[0], m = sizes[1];
-    // The kernel reads nodes[i] for i < n and triangles[j] for j < m only; validate so it cannot fault.
-    if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
+    if (int rc = rt_host_check_bvh_sizes(sizes, n_nodes, n_tris, n_mats)) return rc;
     if ((n && !nodes32) || (m && !tris64) || (n_mats && !mats32)) return fail(RT_ERR_ARG, "rt_set_bvh: null buffer");
-    if (n > (1u << 30)) return fail(RT_ERR_ARG, "rt_set_bvh: tree too large");
-    // Tree::build (tree.rs:38) makes n = m.next_power_of_two() (>= 1); the walks rely on it (leaf pairs: the
-    // children of nodes n/2 .. n-1 are leaves)
-    if (n == 0 || (n & (n - 1u)) != 0) return fail(RT_ERR_ARG, "rt_set_bvh: sizes[0] must be a power of two");
-    if (n_mats >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_bvh: more than 2^28 materials");
     const hrt::Triangle* T = (const hrt::Triangle*)tris64;
     std::vector<hrt_dev::TriDev> td(m);
     for (uint32_t j = 0; j < m; j++) {
@@ -967,6 +1050,29 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->bvh_n = n;
     r->bvh_m = m;
+    return RT_OK;
+}
+
+int rt_host_check_bvh_sizes(const uint32_t sizes[2], uint32_t n_nodes, uint32_t n_tris, uint32_t n_mats) {
+    if (!sizes) return fail(RT_ERR_ARG, "rt_set_bvh: null sizes");
+    const uint32_t n = sizes[0], m = sizes[1];
+    // The kernel reads nodes[i] for i < n and triangles[j] for j < m only; validate so it cannot fault.
+    if (n_nodes < n || n_tris < m) return fail(RT_ERR_ARG, "rt_set_bvh: sizes exceed the buffers given");
+    // Tree::build (tree.rs:38) makes n = m.next_power_of_two() (>= 1); the walks rely on it (leaf pairs: the
+    // children of nodes n/2 .. n-1 are leaves)
+    if (n == 0 || (n & (n - 1u)) != 0) return fail(RT_ERR_ARG, "rt_set_bvh: sizes[0] must be a power of two");
+    // The walks load nodes (32 B) and triangles (64 B) through buffer descriptors with 32-bit byte sizes and
+    // offsets (rt_kernels.hip node_hit_top, tri_test<TBUF>): n x 32 and m x 64 must stay below 2^32.
+    if (n > RT_MAX_TREE_NODES) return fail(RT_ERR_ARG, "rt_set_bvh: more than RT_MAX_TREE_NODES (2^26) nodes");
+    if (m >= (1u << 26)) return fail(RT_ERR_ARG, "rt_set_bvh: 2^26 or more triangles");
+    if (n_mats >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_bvh: more than 2^28 materials");
+    return RT_OK;
+}
+
+int rt_testing_set_faults(rt_renderer* r, uint32_t ring_slots_max, uint32_t fail_alloc_above_mb) {
+    if (!r) return fail(RT_ERR_ARG, "rt_testing_set_faults: null");
+    r->test_ring_slots_max = ring_slots_max;
+    r->test_fail_alloc_above_mb = fail_alloc_above_mb;
     return RT_OK;
 }
 
@@ -1049,7 +1155,6 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (ds.rc) return ds.rc;
     r->width = std::max<uint32_t>(1, width);  // renderer.rs:274-275
     r->height = std::max<uint32_t>(1, height);
-    if (r->params.row0 >= r->height) r->params.row0 = 0;
     r->frame_count = 0;
     return zero_image(r);
 }
@@ -1072,6 +1177,7 @@ int rt_release_scratch(rt_renderer* r) {
     }
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->samples.release();
+    r->samples2.release();
     r->ring.release();
     r->ring_ctl.release();
     return RT_OK;

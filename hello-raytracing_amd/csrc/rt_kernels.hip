@@ -325,7 +325,12 @@ __device__ __forceinline__ void load_hnode(const uint4* __restrict__ hn, uint32_
     n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
 }
 
-template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256>
+// NOOVF: the stack cannot overflow — a tree of depth <= STACK (renderer.cpp gates k_trace_split<LNODES> and the
+// mixed kernels' 8-entry stack on depth <= 8): visiting a node of depth d the stack holds at most d entries (one
+// pending sibling per level above it), so a push at an internal node (d <= depth - 1) leaves at most depth. The
+// push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
+template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
+          bool NOOVF = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
     const float4* __restrict__ nodes = P.bvh_nodes;
@@ -364,11 +369,21 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             const bool hr = SELECT ? padded_box_hit_nb(n2, n3, S, bt, tr) : padded_box_hit(n2, n3, S, bt, tr);
             tally.boxes += 2;
             const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
-            if constexpr (SELECT) {
+            if constexpr (SELECT && NOOVF) {
+                // (updates written unconditionally: the node and stack depth stay in one register each across the
+                // descent loop instead of being copied at its head)
+                const bool lfirst = hl && (!hr || tl <= tr);
+                const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
+                const bool both = hl && hr, any = hl || hr;
+                if (both) stack[sp * LS] = far;
+                sp += both ? 1 : 0;
+                node = any ? near : node;
+                if (any) continue;
+            } else if constexpr (SELECT) {
                 const bool lfirst = hl && (!hr || tl <= tr);
                 const uint32_t near = lfirst ? left : right, far = lfirst ? right : left;
                 if (hl && hr) {
-                    if (sp < STACK) {
+                    if (NOOVF || sp < STACK) {
                         stack[sp * LS] = far;
                         sp++;
                     } else {
@@ -461,11 +476,12 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
-template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256, bool KA = false>
+template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256, bool KA = false, bool NOOVF = false>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin<H16, false, KA>(P, r, best, Q, tally)) bvh_run<false, STACK, false, H16, LS>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
+    if (bvh_begin<H16, false, KA>(P, r, best, Q, tally))
+        bvh_run<false, STACK, false, H16, LS, NOOVF>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
     return bvh_end<KA>(P, r, Q, best, tally);
 }
 
@@ -715,10 +731,13 @@ __device__ __forceinline__ void walk_bvh(const KParams& P, const Ray& r, float& 
 // overflow falls back to the reference walk.
 constexpr int TRI_STACK = 24;
 
-__device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& best, int& bj, Tally& tally,
+// (the SAH tree's constants are read through kargs() where they are used, not held in SGPRs across the persistent
+// loop: the mixed kernels with this walk spilled 2-10 SGPRs otherwise)
+__device__ __forceinline__ void walk_sah(const KParams& /*P*/, const Ray& r, float& best, int& bj, Tally& tally,
                                          uint32_t* stack) {
-    const f3 op = mk(r.o.x - P.tb_rc[0], r.o.y - P.tb_rc[1], r.o.z - P.tb_rc[2]);
-    const float D = __builtin_amdgcn_sqrtf(dot(op, op)) * 1.001f + P.tb_rr_h;
+    const KPtr P = kargs();
+    const f3 op = mk(r.o.x - P->tb_rc[0], r.o.y - P->tb_rc[1], r.o.z - P->tb_rc[2]);
+    const float D = __builtin_amdgcn_sqrtf(dot(op, op)) * 1.001f + P->tb_rr_h;
     const float pad = D * 0x1p-12f;
     Slab S;
     S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
@@ -726,13 +745,13 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
     S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
     S.lo = S.lo * S.inv;
     S.hi = S.hi * S.inv;
-    uint32_t node = P.tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
+    uint32_t node = P->tb_root;  // bj: index of the best triangle (-1: none, or the best is a sphere)
     int sp = 0;
     uint32_t overflow = 0u;  // an integer, not an i1 lane mask (see bvh_run)
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
             float4 n0, n1, n2, n3;
-            load_hnode(P.tb_hnodes, node, n0, n1, n2, n3);
+            load_hnode(P->tb_hnodes, node, n0, n1, n2, n3);
             float tl, tr;
             const bool hl = padded_box_hit(n0, n1, S, best, tl);
             const bool hr = padded_box_hit(n2, n3, S, best, tr);
@@ -754,8 +773,8 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
         } else {
             const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
             for (uint32_t k = 0; k < cnt; k++) {
-                const uint32_t j = P.tb_order[first + k];
-                const float t = tri_t(r, P.tris[j]);
+                const uint32_t j = P->tb_order[first + k];
+                const float t = tri_t(r, P->tris[j]);
                 tally.tris++;
                 if (t >= 1e-4f && (t < best || (t == best && bj >= 0 && (int)j < bj))) {
                     best = t;
@@ -767,14 +786,14 @@ __device__ __forceinline__ void walk_sah(const KParams& P, const Ray& r, float& 
         node = stack[(--sp) * 256];
     }
     if (overflow != 0u) {  // a dropped subtree: finish with the lexicographic minimum over every triangle
-        for (uint32_t j = 0; j < P.m; j++) {
-            const float t = tri_t(r, P.tris[j]);
+        for (uint32_t j = 0; j < P->m; j++) {
+            const float t = tri_t(r, P->tris[j]);
             if (t >= 1e-4f && (t < best || (t == best && bj >= 0 && (int)j < bj))) {
                 best = t;
                 bj = (int)j;
             }
         }
-        tally.tris += P.m;
+        tally.tris += P->m;
     }
 }
 
@@ -785,7 +804,8 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
     int bi = -1, bj = -1;  // winning sphere slot / triangle index
     if (MODE != MODE_TRIS) {
         if constexpr (SCAN == SCAN_BVH) {
-            bi = scan_spheres_bvh(P, r, best, (uint32_t*)lds, tally);
+            // (with the SAH triangle walk the sphere walk's rare-path constants are read through kargs(): 0 SGPR spills)
+            bi = scan_spheres_bvh<BVH_STACK, true, 256, TSAH>(P, r, best, (uint32_t*)lds, tally);
         } else if constexpr (SCAN == SCAN_DEFER) {
             bi = scan_spheres_deferred(P, r, best, (uint16_t*)lds);
             tally.spheres += P.nslots;
@@ -1401,7 +1421,7 @@ __device__ __forceinline__ bool steal_scan(const WaveJobs& J, uint32_t lane, uin
 // nothing claimed; then steal_drained() tells whether no frame is left unclaimed anywhere — none can appear (jobs
 // come only from the drained queue), so the caller stops asking — or an open slot was seen whose claim lost a
 // race (ask again later).
-__device__ __forceinline__ bool steal_block(const WaveJobs& J, uint32_t lane, uint32_t& tile, uint32_t& frame) {
+__device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t lane, uint32_t& tile, uint32_t& frame) {
     const uint32_t priv = J.get(WJ_PRIV_N);
     if (priv != 0u) {
         frame = J.get(WJ_PRIV_F);
@@ -1439,6 +1459,11 @@ __device__ __forceinline__ bool steal_block(const WaveJobs& J, uint32_t lane, ui
     J.set(WJ_ST, ST_QEMPTY);  // (clears ST_RETRY)
     return steal_scan(J, lane, tile, frame);
 }
+__device__ __forceinline__ bool steal_block(const WaveJobs& J, uint32_t lane, uint32_t& tile, uint32_t& frame) {
+    const bool got = steal_block_claim(J, lane, tile, frame);
+    if (got) J.set(WJ_IDLE, 0u);  // idle_spin's watchdog counts CONSECUTIVE rounds without work (lost races)
+    return got;
+}
 __device__ __forceinline__ bool steal_drained(const WaveJobs& J) { return (J.get(WJ_ST) & ST_RETRY) == 0u; }
 
 // Refill with primary rays by frame block (k_trace with the simple sphere scan): when the wave's block
@@ -1473,7 +1498,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
             B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             if (B.pr_ok) {
-                const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
+                const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, P.kr0 + kr);
                 const Ray pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
                 B.pr_o = pr.o;
                 B.pr_d = pr.d;
@@ -1524,7 +1549,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool valid = x < P.W && kr < P.nrows;
-    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
+    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, P.kr0 + kr);
     float* px = P.image + ((size_t)kr * P.W + x) * 3u;
 
     float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
@@ -1732,12 +1757,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t l = sid & 63u;
                 fl = sample_ref(J, job_f0, sid >> 6);
                 pix = job_tile * 64u + l;
-                const uint32_t x = (job_tile % P.tiles_w) * 8u + (l & 7u);
-                const uint32_t kr = (job_tile / P.tiles_w) * 8u + (l >> 3);
+                // (the SAH-walk kernels read the tile map, row map and time through kargs() here: SGPRs)
+#define HRT_KF(f) (TSAH ? kargs()->f : P.f)
+                const uint32_t x = (job_tile % HRT_KF(tiles_w)) * 8u + (l & 7u);
+                const uint32_t kr = (job_tile / HRT_KF(tiles_w)) * 8u + (l >> 3);
                 need = false;
-                if (x < P.W && kr < P.nrows) {  // ragged edge tiles: samples outside the image are skipped
-                    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
-                    ray = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (job_f0 + (sid >> 6)) * P.dtime, s);
+                if (x < HRT_KF(W) && kr < HRT_KF(nrows)) {  // ragged edge tiles: samples outside the image are skipped
+                    const uint32_t y = global_row(HRT_KF(row0), HRT_KF(row_block), HRT_KF(row_stride), HRT_KF(kr0) + kr);
+                    ray = primary_ray<MODE>(&kargs()->cam, x, y, HRT_KF(time0) + (job_f0 + (sid >> 6)) * HRT_KF(dtime), s);
+#undef HRT_KF
                     sky_t = ray.d.y * 0.5f + 0.5f;
                     att = mk(1.0f, 1.0f, 1.0f);
                     bounce = 0;
@@ -1879,7 +1907,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
             uint32_t ps = 0;
             if (pok) {
-                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
+                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, K->kr0 + kr);
                 pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
             }
             blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
@@ -2030,7 +2058,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 uint32_t ps = 0;
                 if (pok) {
                     const KPtr K = kargs();  // row map and time: loaded here, not held in SGPRs
-                    const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
+                    const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, K->kr0 + kr);
                     pr = primary_ray<MODE>(&K->cam, x, y, K->time0 + (job_f0 + blk_f) * K->dtime, ps);
                 }
                 blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
@@ -2088,8 +2116,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_PHASE(1);
         HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
-            if constexpr (LNODES) {
-                if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
+            if constexpr (LNODES) {  // (depth <= LNODE_DEPTH = SPLIT_STACK: no overflow)
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
             } else {
                 if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
                     qs = 2u;
@@ -2167,13 +2195,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // suspends the heap walk once fewer than `suspend_below` lanes are still walking, so lanes whose rays
 // miss the mesh (one node test) do not idle behind the wave's longest walk (C4: 7.0 -> 8.2 Grays/s;
 // C5: 6.25 -> 6.55). Bit-identical to k_trace, with the same node/triangle counts.
-// HL: the heap's top in LDS (renderer.cpp decides: m <= 65535, and with the culling BVH a sphere tree of depth
-// <= 8). 0: none, 256-lane workgroups and 32-bit triangle lists; 1-3: the deferred-triangle list holds 16-bit
-// indices and shares its words with an 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves
-// per SIMD: 1 = nodes 1..255 (8 levels, 8 KB) with 256-lane workgroups, 2 = nodes 1..511 (9 levels, 16 KB) with 512,
-// 3 = nodes 1..991 (almost 10 levels, 31 KB) with 768 (two workgroups per CU: 78 KB each).
-constexpr uint32_t heap_wg(int hl) { return hl == 2 ? 512u : hl == 3 ? 768u : 256u; }
-constexpr uint32_t heap_top_n(int hl) { return hl == 0 ? 0u : hl == 1 ? 256u : hl == 2 ? 512u : 992u; }
+// HL: the heap's top in LDS (renderer.cpp decides: rt_params.heap_lds not 1 (off), and with the culling BVH a
+// sphere tree of depth <= 8, whose walk fits the 8-entry stack). 0: none, 256-lane workgroups, a 16-entry leaf-pair
+// list per lane; 1, 3: an 8-entry leaf-pair list (32-bit entries: j0 | PAIR_BIT) that shares its words with the
+// 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves per SIMD: 3 = nodes 1..991 (almost 10
+// levels, 31 KB) with 768-lane workgroups (two per CU: 78 KB each), the default; 1 = nodes 1..255 (8 levels, 8 KB)
+// with 256-lane workgroups, only for the mixed program's deferred sphere scan (its candidate lists assume 256 lanes).
+// (Nodes 1..511 with 512-lane workgroups, measured between the two in round 3, was retired.)
+constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
+constexpr uint32_t heap_top_n(int hl) { return hl == 0 ? 0u : hl == 1 ? 256u : 992u; }
 
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
@@ -2238,7 +2268,8 @@ k_trace_split_tris(const KParams P) {
                 qs = 3u;
             } else {
                 float sb = FLT_MAX_REF;
-                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true>(P, ray, sb, sstack, tally);
+                // (HL > 0: renderer.cpp runs these only for sphere trees of depth <= 8 = SPHERE_STACK: no overflow)
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true, (HL > 0)>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
@@ -2446,42 +2477,45 @@ static hipError_t launch_split_tris_hl(const KParams& P, hipStream_t stream) {
 template <int MODE, int SCAN>
 static hipError_t launch_split_tris(const KParams& P, hipStream_t stream) {
     if constexpr (SCAN == SCAN_DEFER) {  // (its deferred-scan lists assume 256-lane workgroups)
+        if (P.tri_small > 1u) return hipErrorInvalidValue;
         return P.tri_small ? launch_split_tris_hl<MODE, SCAN, 1>(P, stream) : launch_split_tris_hl<MODE, SCAN, 0>(P, stream);
     } else {
-        switch (P.tri_small) {
-        case 1: return launch_split_tris_hl<MODE, SCAN, 1>(P, stream);
-        case 2: return launch_split_tris_hl<MODE, SCAN, 2>(P, stream);
-        case 3: return launch_split_tris_hl<MODE, SCAN, 3>(P, stream);
-        default: return launch_split_tris_hl<MODE, SCAN, 0>(P, stream);
-        }
+        if (P.tri_small != 0u && P.tri_small != 3u) return hipErrorInvalidValue;
+        return P.tri_small ? launch_split_tris_hl<MODE, SCAN, 3>(P, stream) : launch_split_tris_hl<MODE, SCAN, 0>(P, stream);
     }
 }
 
 // Sample queue, part 1: trace every sample of the chunk into P.samples.
 // variant: SCAN_SIMPLE, SCAN_DEFER or SCAN_BVH (resolved by the host); P.tri_bvh picks the triangle walk.
+// The reference heap walk (triangle / mixed programs) and the sphere program's culling BVH always run in the
+// suspendable-walk kernels (renderer.cpp sets suspend_below >= 1 for them; 1 = a wave never leaves a walk early);
+// k_trace is instantiated only for what has no split kernel: the sphere program's linear scans and the opt-in SAH
+// triangle walk (tri_bvh = 1).
 template <int MODE, bool TSAH>
 static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t stream) {
     if constexpr (MODE != MODE_SPHERE && !TSAH) {
-        if (P.suspend_below > 0u) {
-            // The mixed program with the culling BVH runs its sphere walk to completion in the begin phase
-            // (stack in the triangle-batch LDS) and suspends only the heap walk: C5 at 256 spp 6.25 -> 6.55
-            // Grays/s. (Splitting both walks measured 5.93; an earlier heap-only form with the stack in
-            // the LDS block region, 6.05.)
-            if constexpr (MODE == MODE_TRIS) {
-                return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
-            } else {
-                if (variant == SCAN_SIMPLE) return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
-                if (variant == SCAN_DEFER) return launch_split_tris<MODE, SCAN_DEFER>(P, stream);
-                return launch_split_tris<MODE, SCAN_BVH>(P, stream);
-            }
+        if (P.suspend_below == 0u) return hipErrorInvalidValue;
+        // The mixed program with the culling BVH runs its sphere walk to completion in the begin phase
+        // (stack in the triangle-batch LDS) and suspends only the heap walk: C5 at 256 spp 6.25 -> 6.55
+        // Grays/s. (Splitting both walks measured 5.93; an earlier heap-only form with the stack in
+        // the LDS block region, 6.05.)
+        if constexpr (MODE == MODE_TRIS) {
+            return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
+        } else {
+            if (variant == SCAN_SIMPLE) return launch_split_tris<MODE, SCAN_SIMPLE>(P, stream);
+            if (variant == SCAN_DEFER) return launch_split_tris<MODE, SCAN_DEFER>(P, stream);
+            return launch_split_tris<MODE, SCAN_BVH>(P, stream);
         }
-    }
-    if constexpr (MODE == MODE_TRIS) {
+    } else if constexpr (MODE == MODE_TRIS) {
         return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
     } else {
         if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
         if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream, kname("k_trace", MODE, SCAN_DEFER, (int)TSAH));
-        return launch_persistent(k_trace<MODE, SCAN_BVH, TSAH>, P, stream, kname("k_trace", MODE, SCAN_BVH, (int)TSAH));
+        if constexpr (MODE == MODE_SPHERE) {
+            return hipErrorInvalidValue;  // the culling BVH runs in k_trace_split
+        } else {
+            return launch_persistent(k_trace<MODE, SCAN_BVH, TSAH>, P, stream, kname("k_trace", MODE, SCAN_BVH, (int)TSAH));
+        }
     }
 }
 

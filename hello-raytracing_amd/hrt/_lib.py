@@ -45,8 +45,6 @@ class RtParams(C.Structure):
         ("suspend_below", C.c_uint32),
         ("row_block", C.c_uint32),
         ("fold", C.c_uint32),
-        ("ring_slots_max", C.c_uint32),
-        ("fail_alloc_above_mb", C.c_uint32),
         ("heap_lds", C.c_uint32),
         ("steal", C.c_uint32),
         ("tail_split", C.c_uint32),
@@ -72,7 +70,7 @@ class RtStats(C.Structure):
         ("kernel", C.c_char * 64),
         ("fold_bytes", C.c_uint64),
         ("fold_ring", C.c_uint32),
-        ("pad_stats", C.c_uint32),
+        ("bands", C.c_uint32),
         ("device_bytes", C.c_uint64),
     ]
 
@@ -110,6 +108,7 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),
     "rt_build_info": (C.c_char_p, []),
+    "rt_host_check_bvh_sizes": (C.c_int, [_PU32, _U32, _U32, _U32]),
     "rt_host_camera_new": (C.c_int, [_PF, _PF, C.c_float, C.c_float, C.c_float, C.c_char_p]),
     "rt_host_mesh_load_obj": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.POINTER(_P)]),
     "rt_host_mesh_counts": (C.c_int, [_P, _PU32, _PU32]),
@@ -128,6 +127,11 @@ SIGNATURES = {
         C.c_int,
         [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_float, C.POINTER(C.c_int), _PF],
     ),
+}
+
+# include/hrt_testing.h: test-only entry points (fault injection), not part of the drop-in surface.
+TESTING_SIGNATURES = {
+    "rt_testing_set_faults": (C.c_int, [_P, _U32, _U32]),
 }
 
 _lib = None
@@ -149,7 +153,7 @@ def lib() -> C.CDLL:
                 "(or __graft_entry__.build()); the renderer has no Python/CPU fallback"
             )
         L = C.CDLL(os.fspath(LIB_PATH))
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in {**SIGNATURES, **TESTING_SIGNATURES}.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

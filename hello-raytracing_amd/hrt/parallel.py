@@ -93,3 +93,21 @@ def gather_image(part, height: int, dist, rank: int, world: int, dst: int = 0, g
     if rank != dst:
         return None
     return assemble(gathered, height, world, out, block=block)
+
+
+def image_checksum(img, rows, width: int) -> int:
+    """Position-dependent checksum of image rows: sum over the f32 words w at global flat index g of
+    w * (2g + 1) (mod 2^64, as a signed int64). `img` holds the rows `rows` (global indices, local order) of an
+    image `width` pixels wide, 3 words per pixel (extra padding rows beyond len(rows) are ignored). Additive over
+    disjoint row sets, so the gathered image's checksum on the destination rank equals the sum of the ranks' local
+    checksums exactly when every rank's words arrived at the right place (bench.py, multi-rank runs)."""
+    import torch
+
+    n = len(rows)
+    if n == 0:
+        return 0
+    words = img[:n].reshape(n, width * 3).contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    r = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=words.device)[:, None]
+    g = r * (width * 3) + torch.arange(width * 3, dtype=torch.int64, device=words.device)[None, :]
+    return int((words * (2 * g + 1)).sum().item())
+

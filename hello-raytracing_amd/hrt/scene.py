@@ -333,9 +333,16 @@ class Renderer:
 
     def set_params(self, **kw) -> None:
         p = self.params
+        names = {f[0] for f in RtParams._fields_}
         for k, v in kw.items():
+            if k not in names:  # (a ctypes Structure would silently take an unknown attribute)
+                raise TypeError(f"set_params: rt_params has no field {k!r}")
             setattr(p, k, v)
         check(lib().rt_set_params(self._h, C.byref(p)), "set_params")
+
+    def set_faults(self, ring_slots_max: int = 0, fail_alloc_above_mb: int = 0) -> None:
+        """Test-only fault injection (include/hrt_testing.h rt_testing_set_faults)."""
+        check(lib().rt_testing_set_faults(self._h, ring_slots_max, fail_alloc_above_mb), "testing_set_faults")
 
     @property
     def local_rows(self) -> int:
@@ -415,7 +422,7 @@ def compare_ppm_images(img1: str, img2: str, tolerance_percent: float) -> float:
 
 # ----------------------------------------------------------------------------------------- scenes
 class SceneSphere:
-    """src/scene/scene_sphere.rs + the Scene impl of src/scene/mod.rs:641-680."""
+    """src/scene/scene_sphere.rs + the Scene impl of src/scene/mod.rs:68-107."""
 
     def __init__(self, renderer: Renderer, camera: np.ndarray, objects: list):
         self.renderer = renderer
@@ -471,7 +478,7 @@ class SceneSphere:
 
 
 class SceneTris:
-    """src/scene/scene_tris.rs + the Scene impl of src/scene/mod.rs:600-639."""
+    """src/scene/scene_tris.rs + the Scene impl of src/scene/mod.rs:27-66."""
 
     def __init__(self, renderer: Renderer, camera: np.ndarray, tris_bvh: Tree):
         self.renderer = renderer

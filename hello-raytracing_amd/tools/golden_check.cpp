@@ -128,7 +128,7 @@ int main(int argc, char** argv) {
             std::fprintf(stderr, "rt_create: %s\n", rt_last_error());
             return 3;
         }
-        // Scene::init (mod.rs:641-645): set_camera + write_scene_data (truncated to MAX_OBJECT_IN_SCENE)
+        // Scene::init (mod.rs:69-72): set_camera + write_scene_data (scene_sphere.rs:24-31) (truncated to MAX_OBJECT_IN_SCENE)
         const uint32_t n = (uint32_t)std::min<size_t>(sc.objects.size(), RT_MAX_OBJECT_IN_SCENE);
         if (rt_set_camera(r, sc.camera) || rt_set_spheres(r, sc.objects.data(), n)) return 3;
         for (uint32_t i = 0; i < frames; i++) {  // rendering_tests.rs:22-25

@@ -71,9 +71,11 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; 32768. The sample buffer when it holds
-                                  min(frames, 320) frames of colours (launches of as many frames as it
-                                  holds), else the fold ring in this budget (bounded memory, slower)     */
+    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; default 8192. The sample buffer: one launch
+                                  when a draw's colours fit; else bands of tile rows x every frame in two
+                                  buffers of half the budget, pipelined over two streams; else launches of
+                                  as many frames as fit, or the fold ring below min(frames, 320) frames
+                                  (bounded memory, slower)                                 */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
                                   power of two (at most 1024); default 0 = per kernel: 32 with the
                                   suspendable walks, 16 for the linear sphere scans                      */
@@ -84,9 +86,9 @@ typedef struct rt_params {
     uint32_t suspend_below;    /* sample queue: a wave suspends its walks (sphere culling BVH of the sphere
                                   program; reference heap walk of the triangle / mixed programs) once
                                   fewer than this many of its 64 lanes are still walking, so finished
-                                  lanes shade and start their next query instead of idling (0 = every
-                                  query runs to completion, k_trace); default 24 (sphere) / 32 (others);
-                                  not used by the mixed program with the culling BVH or tri_bvh = 1.
+                                  lanes shade and start their next query instead of idling (0 = no wave
+                                  leaves a walk before all of its lanes finish); default 24 (sphere) / 32
+                                  (others); not used by tri_bvh = 1 or the linear sphere scans.
                                   Bit-identical either way                      */
     uint32_t row_block;        /* rows per block of the row partition (default 1; 0 reads as 1): the renderer
                                   owns rows row0 + k*row_step*row_block + j, j < row_block, in that order.
@@ -94,13 +96,9 @@ typedef struct rt_params {
                                   8-row tile rows dealt round-robin (bench.py)            */
     uint32_t fold;             /* sample queue colour fold: 0 auto (by queue_budget_mb, above), 1 the sample
                                   buffer + k_accumulate, 2 the fold ring (bounded memory); bit-identical */
-    uint32_t ring_slots_max;   /* fold ring: at most this many job slots (a power of two; 0 = no cap).
-                                  Tests: with few slots nearly every job waits for one                    */
-    uint32_t fail_alloc_above_mb; /* fault injection for tests: colour-fold allocations above this many MiB
-                                  fail as a refused hipMalloc would (0 = off); the draw then shrinks them */
-    uint32_t heap_lds;         /* triangle / mixed programs: 0 auto = nodes 1..991 of the implicit heap in LDS
-                                  (k_trace_split_tris<.., HL = 3>), 1 off (every node from L1/L2), 2 / 3 / 4 =
-                                  nodes 1..255 / 1..511 / 1..991; bit-identical always                      */
+    uint32_t heap_lds;         /* triangle / mixed programs: the top of the implicit heap in LDS, 0 auto = on,
+                                  1 off (every node from L1/L2), 2 on: nodes 1..991 (768-lane workgroups;
+                                  nodes 1..255 with the deferred sphere scan); bit-identical always        */
     uint32_t steal;            /* sample queue with the sample buffer, suspendable-walk kernels: frame-block work
                                   stealing (a wave whose job queue is drained claims single frames of other
                                   waves' jobs, so no long job trails the launch): 0 auto = on for launches of
@@ -142,7 +140,8 @@ typedef struct rt_stats {
                               job_frames x 64 px x 16 B plus control words); 0 for the tiles schedule    */
     uint32_t fold_ring;    /* 1: the last draw folded through the fold ring (bounded memory), 0: through the
                               sample buffer and k_accumulate (rt_params.queue_budget_mb decides)         */
-    uint32_t pad_stats;
+    uint32_t bands;        /* sample buffer: row bands the last draw's launches covered (1 = every launch covers all
+                              of the renderer's rows; > 1 = pipelined band launches, rt_params.queue_budget_mb) */
     uint64_t device_bytes; /* device memory the renderer holds after the last draw call (image, scene,
                               colour fold, counters): the fold's share stays within queue_budget_mb      */
 } rt_stats;
@@ -162,9 +161,12 @@ int rt_set_camera(rt_renderer *r, const void *camera80);
 int rt_set_spheres(rt_renderer *r, const void *spheres48, uint32_t n);
 /* SceneTris::write_tree_data — scene_tris.rs:21-44 (group1 bindings 0..3): sizes = [n, m] (bvh_tree_size),
  * n Node (index 0 unused), m Triangle, k Material. n must be a power of two, as Tree::build makes it
- * (tree.rs:38, m.next_power_of_two()); RT_ERR_ARG otherwise. */
+ * (tree.rs:38, m.next_power_of_two()), and at most RT_MAX_TREE_NODES (the kernels read nodes and triangles
+ * through buffer descriptors with 32-bit byte offsets: n x 32 B and m x 64 B stay below 4 GiB); RT_ERR_ARG
+ * otherwise (rt_host_check_bvh_sizes applies the same rules without a device). */
 int rt_set_bvh(rt_renderer *r, const uint32_t sizes[2], const void *nodes32, uint32_t n_nodes,
                const void *tris64, uint32_t n_tris, const void *mats32, uint32_t n_mats);
+#define RT_MAX_TREE_NODES (1u << 26) /* 2^26 nodes (2 GiB), up to 2^26 - 1 triangles (4 GiB)            */
 
 /* Renderer::set_time / set_frame_count — renderer.rs:315-323. */
 int rt_set_time(rt_renderer *r, uint32_t time);
@@ -194,9 +196,12 @@ int rt_synchronize(rt_renderer *r);
 int rt_get_stats(const rt_renderer *r, rt_stats *out);
 /* Frees the sample queue's colour-fold memory (the sample buffer or the fold ring, rt_stats.fold_bytes)
  * after the pending draws; the next queue draw allocates it again. For a renderer kept alive between
- * renders beside other work: the 32 GiB default budget lets one C3 render hold 25.5 GB (no reference
+ * renders beside other work: the default 8 GiB budget lets one C3 render hold 7.6 GB (no reference
  * counterpart: wgpu frees nothing either, but the reference has no per-sample buffer). */
 int rt_release_scratch(rt_renderer *r);
+
+/* Test-only entry points (fault injection) are declared in hrt_testing.h, not here: they are not part of
+ * the drop-in surface. */
 
 /* Raw per-draw device counters (no reference counterpart; diagnostics). Slots 0-4 are the rt_stats
  * work counters; in the diagnostic build (rt_diagnostic_build() == 1, lib/libhrt_diag.so) slots 8-11
@@ -238,11 +243,15 @@ int rt_host_mesh_load_obj(const char *data, size_t len, const void *material32, 
 int rt_host_mesh_counts(const rt_mesh *m, uint32_t *n_vertices, uint32_t *n_indices);
 int rt_host_mesh_destroy(rt_mesh *m);
 
+/* The size rules rt_set_bvh applies (sizes [n, m], buffer lengths, materials), without a device: RT_OK or
+ * RT_ERR_ARG with rt_last_error() naming the rule. */
+int rt_host_check_bvh_sizes(const uint32_t sizes[2], uint32_t n_nodes, uint32_t n_tris, uint32_t n_mats);
+
 /* Tree::new / Tree::add_mesh / Tree::build — src/scene/bvh/tree.rs:20-90. */
 int rt_host_tree_new(rt_tree **out);
 int rt_host_tree_add_mesh(rt_tree *t, const rt_mesh *m);
 int rt_host_tree_build(rt_tree *t);
-/* Tree::build on `threads` host threads (0 = HRT_HOST_THREADS or min(16, cores); rt_host_tree_build uses 0).
+/* Tree::build on `threads` host threads (0 = min(16, cores); rt_host_tree_build uses 0).
  * Level-synchronous BFS with concurrent stable sorts: byte-identical to the sequential build. */
 int rt_host_tree_build_threads(rt_tree *t, int threads);
 /* Views into the tree (valid until the next mutation): sizes [n, m], n nodes, m triangles, k materials. */

@@ -47,6 +47,13 @@
  *   4: contracts 2 and 3 together;
  *   5: every division by a computed value as a * (1 / b) (the reciprocal-based division GPU compilers emit
  *      for WGSL's 2.5-ulp `/`), normalize included.
+ * Hardware-approximate forms a WGSL compiler may emit, alone (6-8) and together (9):
+ *   6: pow(x, 5) of reflectance (shader_sphere.wgsl:166-171) as exp2(5 * log2(x)) (libm exp2f / log2f);
+ *   7: normalize(v) (every site: make_ray's 4-D normalise, the AA and disk vectors, hemisphere, scatter) as
+ *      v * rsq(dot(v, v)) with a 1-ulp rsq: the correctly rounded 1/sqrt moved by -1, 0 or +1 ulp, chosen by a
+ *      hash of the operand's bits (a deterministic stand-in for an unknown hardware rsq);
+ *   8: tan(fov / 2) of make_ray (:124) as sin * (1 / cos) in f32 (not correctly rounded);
+ *   9: 6 + 7 + 8.
  */
 #ifndef ORACLE_CONTRACT
 #define ORACLE_CONTRACT 0
@@ -55,11 +62,29 @@
 #define OC_FUSE (ORACLE_CONTRACT == 2 || ORACLE_CONTRACT == 4)
 #define OC_RCPNORM (ORACLE_CONTRACT == 3 || ORACLE_CONTRACT == 4 || ORACLE_CONTRACT == 5)
 #define OC_RCPDIV (ORACLE_CONTRACT == 5)
+#define OC_POWEXP (ORACLE_CONTRACT == 6 || ORACLE_CONTRACT == 9)
+#define OC_RSQNORM (ORACLE_CONTRACT == 7 || ORACLE_CONTRACT == 9)
+#define OC_TANSC (ORACLE_CONTRACT == 8 || ORACLE_CONTRACT == 9)
 static inline float fmaf_c(float a, float b, float c) { return OC_NOFMA ? a * b + c : fmaf(a, b, c); }
 /* a*b + c at the sites a compiler may fuse */
 static inline float madd(float a, float b, float c) { return OC_FUSE ? fmaf(a, b, c) : a * b + c; }
 /* a / b at the sites whose divisor is computed */
 static inline float divf(float a, float b) { return OC_RCPDIV ? a * (1.0f / b) : a / b; }
+/* contract 7: a 1-ulp reciprocal square root (correctly rounded 1/sqrt(a), moved by -1 / 0 / +1 ulp by a hash of
+ * a's bits), the scale normalize multiplies by */
+static inline float rsq_1ulp(float a) {
+    float r = (float)(1.0 / sqrt((double)a));
+    uint32_t u;
+    memcpy(&u, &a, 4);
+    u = (u ^ (u >> 16)) * 0x45d9f3bu;
+    u ^= u >> 16;
+    const int k = (int)(u % 3u) - 1;
+    if (k > 0) r = nextafterf(r, INFINITY);
+    if (k < 0) r = nextafterf(r, 0.0f);
+    return r;
+}
+/* v_i / |v| at a normalize site, |v|^2 = ss (contract 7: v_i * rsq(ss)) */
+static inline float nrm_div(float vi, float ss, float len) { return OC_RSQNORM ? vi * rsq_1ulp(ss) : vi / len; }
 
 enum { MODE_SPHERE = 0, MODE_TRIS = 1, MODE_MIXED = 2 };
 
@@ -96,6 +121,7 @@ static inline v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
 static inline float dot3(v3 a, v3 b) { return fmaf_c(a.z, b.z, fmaf_c(a.y, b.y, a.x * b.x)); }
 static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
 static inline v3 norm3(v3 a) {
+    if (OC_RSQNORM) { float q = rsq_1ulp(dot3(a, a)); return V(a.x * q, a.y * q, a.z * q); }
     float l = len3(a);
     if (OC_RCPNORM) { float r = 1.0f / l; return V(a.x * r, a.y * r, a.z * r); }
     return V(a.x / l, a.y / l, a.z / l);
@@ -144,13 +170,16 @@ static ray_t make_ray(const o_scene *sc, float ux, float uy, uint32_t *s) {
         float xx = (c->right[i] * ux) * sc->k;
         v[i] = madd(c->up[i] * uy, sc->k, xx) + c->dir[i];
     }
-    float l = sqrtf(fmaf_c(v[3], v[3], fmaf_c(v[2], v[2], fmaf_c(v[1], v[1], v[0] * v[0]))));
-    for (int i = 0; i < 4; i++) d4[i] = OC_RCPNORM ? v[i] * (1.0f / l) : v[i] / l;
+    float ss = fmaf_c(v[3], v[3], fmaf_c(v[2], v[2], fmaf_c(v[1], v[1], v[0] * v[0])));
+    float l = sqrtf(ss);
+    for (int i = 0; i < 4; i++) d4[i] = OC_RCPNORM ? v[i] * (1.0f / l) : nrm_div(v[i], ss, l);
     for (int i = 0; i < 4; i++) f4[i] = madd(d4[i], c->params[0], c->eye[i]);
     /* random_on_disk: shader_sphere.wgsl:118-122 */
     float r1 = rng_float(s), r2 = rng_float(s);
-    float l2 = sqrtf(fmaf_c(r2, r2, r1 * r1));
-    float vx = OC_RCPNORM ? r1 * (1.0f / l2) : r1 / l2, vy = OC_RCPNORM ? r2 * (1.0f / l2) : r2 / l2;
+    float ss2 = fmaf_c(r2, r2, r1 * r1);
+    float l2 = sqrtf(ss2);
+    float vx = OC_RCPNORM ? r1 * (1.0f / l2) : nrm_div(r1, ss2, l2);
+    float vy = OC_RCPNORM ? r2 * (1.0f / l2) : nrm_div(r2, ss2, l2);
     float rr = rng_float(s) * c->params[1];
     o4[0] = madd(vx, rr, c->eye[0]);
     o4[1] = madd(vy, rr, c->eye[1]);
@@ -163,9 +192,10 @@ static ray_t make_ray(const o_scene *sc, float ux, float uy, uint32_t *s) {
     } else {
         float g[4];
         for (int i = 0; i < 4; i++) g[i] = f4[i] - o4[i];
-        float lg = sqrtf(fmaf_c(g[3], g[3], fmaf_c(g[2], g[2], fmaf_c(g[1], g[1], g[0] * g[0]))));
+        float sg = fmaf_c(g[3], g[3], fmaf_c(g[2], g[2], fmaf_c(g[1], g[1], g[0] * g[0])));
+        float lg = sqrtf(sg);
         r.d = OC_RCPNORM ? V(g[0] * (1.0f / lg), g[1] * (1.0f / lg), g[2] * (1.0f / lg))
-                         : V(g[0] / lg, g[1] / lg, g[2] / lg);
+                         : V(nrm_div(g[0], sg, lg), nrm_div(g[1], sg, lg), nrm_div(g[2], sg, lg));
     }
     return r;
 }
@@ -271,7 +301,8 @@ static inline float reflectance(float cosine, float ref_idx) { /* :166-171, pow(
     r0 = r0 * r0;
     float x = 1.0f - cosine;
     float x2 = x * x;
-    return madd(1.0f - r0, (x2 * x2) * x, r0);
+    float p5 = OC_POWEXP ? exp2f(5.0f * log2f(x)) : (x2 * x2) * x; /* contract 6: pow as exp2(5 log2 x) */
+    return madd(1.0f - r0, p5, r0);
 }
 
 /* scatter: shader_sphere.wgsl:172-217 / shader_tris.wgsl:222-267 (metal: tris reflects the raw d) */
@@ -328,9 +359,10 @@ static v3 sample_pixel(const o_scene *sc, uint32_t W, uint32_t H, uint32_t x, ui
     uint32_t s = (x * H + y) * time;
     float aspect = divf((float)W, (float)H);
     float r1 = rng_float(&s), r2 = rng_float(&s);
-    float l = sqrtf(fmaf_c(r2, r2, r1 * r1));
-    float px = ((float)x + 0.5f) + (OC_RCPNORM ? r1 * (1.0f / l) : r1 / l);
-    float py = ((float)y + 0.5f) + (OC_RCPNORM ? r2 * (1.0f / l) : r2 / l);
+    float ssa = fmaf_c(r2, r2, r1 * r1);
+    float l = sqrtf(ssa);
+    float px = ((float)x + 0.5f) + (OC_RCPNORM ? r1 * (1.0f / l) : nrm_div(r1, ssa, l));
+    float py = ((float)y + 0.5f) + (OC_RCPNORM ? r2 * (1.0f / l) : nrm_div(r2, ssa, l));
     float ux = divf(px, (float)W - 1.0f), uy = divf(py, (float)H - 1.0f);
     ux = madd(2.0f, ux, -1.0f) * aspect;
     uy = madd(2.0f, uy, -1.0f) * -1.0f;
@@ -351,7 +383,8 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
                        float *image, int threads, uint64_t *counts) {
     o_scene sc;
     sc.cam = (const o_camera *)camera80;
-    sc.k = tanf(sc.cam->params[2] * 0.5f);
+    sc.k = OC_TANSC ? sinf(sc.cam->params[2] * 0.5f) * (1.0f / cosf(sc.cam->params[2] * 0.5f)) /* contract 8 */
+                    : tanf(sc.cam->params[2] * 0.5f);
     sc.spheres = (const o_sphere *)spheres48; sc.nslots = spheres48 ? nslots : 0;
     sc.nodes = (const o_node *)nodes32; sc.tris = (const o_triangle *)tris64; sc.mats = (const o_material *)mats32;
     sc.n = sizes ? sizes[0] : 0; sc.m = sizes ? sizes[1] : 0;

@@ -3,7 +3,9 @@
 The reference's goldens (tests/golden/*.ppm) come from an unknown GPU through naga, whose compiler may fuse or
 reassociate float operations. The build's contract (oracle/rt_oracle.c, contract 0) matches the non-glass
 goldens on 99.99 % of u8 channels; this study renders the seven golden scenes (512 x 512, 100 frames,
-time 1000 + 10 i) with the oracle under six contracts and, for contract 0, sorts every channel that differs
+time 1000 + 10 i) with the oracle under ten contracts (0-5: fusion / division / normalize forms; 6-9: the
+hardware-approximate forms a GPU shader compiler may emit for pow, normalize and tan) and, for contract 0, sorts
+every channel that differs
 from the golden by where it lies:
 
 * edge: the pixel sits on a silhouette, shadow boundary or texture edge — some 4-neighbour differs from it by
@@ -12,7 +14,7 @@ from the golden by where it lies:
 * glass: the pixel's primary rays reach a dielectric sphere in the oracle render (DESIGN.md §2: chaotic);
 * interior: neither.
 It also reports how many of those channels are float-fragile: their u8 value changes under at least one of
-the other five contracts — the mismatch then depends on the reference GPU's unknown contract.
+the other contracts — the mismatch then depends on the reference GPU's unknown contract.
 
 usage: python tests/golden/contract_study.py [--out tests/golden/contract_study.json]
 """
@@ -33,7 +35,9 @@ import scenes  # noqa: E402
 
 CONTRACTS = {0: "build contract (FMA in dot / disc / point_on_ray; v / sqrt)", 1: "no FMA at all",
              2: "contract 0 + every a*b+c fused", 3: "contract 0 + normalize as v * (1 / sqrt)",
-             4: "contracts 2 + 3", 5: "every division by a computed value as a * (1 / b)"}
+             4: "contracts 2 + 3", 5: "every division by a computed value as a * (1 / b)",
+             6: "contract 0 + pow(x, 5) as exp2(5 log2 x)", 7: "contract 0 + normalize as v * rsq(v.v), 1-ulp rsq",
+             8: "contract 0 + tan(fov/2) as sin * (1 / cos) in f32", 9: "contracts 6 + 7 + 8"}
 
 
 def edge_mask(golden: np.ndarray) -> np.ndarray:
@@ -102,11 +106,12 @@ def main() -> int:
     a = ap.parse_args()
     res = study()
     Path(a.out).write_text(json.dumps({"contracts": CONTRACTS, "scenes": res}, indent=1))
-    print("| golden | " + " | ".join(f"c{c} exact / max" for c in CONTRACTS)
+    print("| golden | " + " | ".join(f"c{c} exact / max / mean" for c in CONTRACTS)
           + " | c0 mismatched px: edge / glass / interior | c0 mismatched channels float-fragile |")
     print("|---|" + "---|" * (len(CONTRACTS) + 2))
     for name, per in res.items():
-        cells = [f"{per[c]['exact_u8'] * 100:.3f} % / {per[c]['max_abs_du8']}" for c in CONTRACTS]
+        cells = [f"{per[c]['exact_u8'] * 100:.3f} % / {per[c]['max_abs_du8']} / {per[c]['mean_abs_du8_pct']:.3f} %"
+                 for c in CONTRACTS]
         p0 = per[0]
         print(f"| {name} | " + " | ".join(cells) + f" | {p0['edge']} / {p0['glass']} / {p0['interior']} | "
               f"{p0['mismatched_channels_fragile']} of {p0['mismatched_channels']} |")

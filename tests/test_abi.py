@@ -14,8 +14,11 @@ ROOT = Path(__file__).resolve().parents[1]
 HEADER = (ROOT / "include" / "hrt.h").read_text()
 
 
-def declared_functions():
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(rt_\w+)\s*\(", HEADER, re.M)))
+TESTING_HEADER = (ROOT / "include" / "hrt_testing.h").read_text()
+
+
+def declared_functions(text=HEADER):
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(rt_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_the_boundary():
@@ -29,12 +32,55 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     exported = set(re.findall(r"\bT (rt_\w+)", out))
-    missing = [n for n in declared_functions() if n not in exported]
+    missing = [n for n in declared_functions() + declared_functions(TESTING_HEADER) if n not in exported]
     assert not missing, missing
     assert set(_lib.SIGNATURES) == set(declared_functions())
+    assert set(_lib.TESTING_SIGNATURES) == set(declared_functions(TESTING_HEADER))
+    # the public header declares no test-only entry point, and rt_params carries no fault-injection field
+    assert not set(declared_functions(TESTING_HEADER)) & set(declared_functions())
+    assert "fail_alloc" not in HEADER and "ring_slots_max" not in HEADER
     L = hrt.lib()
     for n in declared_functions():
         assert getattr(L, n) is not None
+
+
+def test_bvh_size_rules_without_a_device():
+    """rt_set_bvh's size rules (the walks' buffer descriptors take 32-bit byte sizes and offsets, so
+    n x 32 B and m x 64 B must stay below 4 GiB; n a power of two as Tree::build makes it), checked on the host."""
+    L = hrt.lib()
+
+    def check(n, m, n_nodes=None, n_tris=None, n_mats=1):
+        sizes = (C.c_uint32 * 2)(n, m)
+        return L.rt_host_check_bvh_sizes(sizes, n if n_nodes is None else n_nodes, m if n_tris is None else n_tris,
+                                         n_mats)
+
+    assert check(1024, 979) == _lib.RT_OK                              # Suzanne (tree.rs:121-124)
+    assert check(16, 12) == _lib.RT_OK                                 # cube (tree.rs:107-110)
+    assert check(1 << 26, (1 << 26) - 1) == _lib.RT_OK                 # the largest tree: 2 GiB of nodes, 4 GiB of tris
+    assert check(1 << 27, (1 << 26) + 1) == _lib.RT_ERR_ARG            # n x 32 B would wrap a 32-bit size
+    assert b"RT_MAX_TREE_NODES" in L.rt_last_error()
+    assert check(1 << 26, 1 << 26) == _lib.RT_ERR_ARG                  # m x 64 B would wrap
+    assert check(1000, 979) == _lib.RT_ERR_ARG                         # not a power of two
+    assert check(0, 0) == _lib.RT_ERR_ARG
+    assert check(1024, 979, n_nodes=1023) == _lib.RT_ERR_ARG           # sizes exceed the buffers given
+    assert check(1024, 979, n_tris=978) == _lib.RT_ERR_ARG
+    assert check(1024, 979, n_mats=1 << 28) == _lib.RT_ERR_ARG
+    assert L.rt_host_check_bvh_sizes(None, 1, 1, 1) == _lib.RT_ERR_ARG
+
+
+def test_library_reads_no_environment_knobs():
+    """the product library takes every setting through rt_params / arguments, none from the environment
+    (the diagnostic build, lib/libhrt_diag.so, may read HRT_RING_DUMP). libhrt.so imports no environment accessor
+    (getenv, secure_getenv, environ), so no code in it can read a variable (the HIP runtime it loads reads its own
+    HIP_* / HSA_* settings), and no HRT_-prefixed name is left in its strings."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    imported = set(re.findall(r"\bU (\w+)", out))
+    assert imported, out  # (the scan saw the import table: HIP runtime and libc symbols)
+    assert not imported & {"getenv", "secure_getenv", "__secure_getenv", "environ", "__environ", "getenv_s"}, imported
+    data = _lib.LIB_PATH.read_bytes()
+    names = sorted(set(re.findall(rb"HRT_[A-Z0-9_]{2,}", data)))
+    assert not names, names
 
 
 def _header_struct(name):
@@ -58,7 +104,7 @@ def test_struct_layouts_match_header():
         got = [(f, t) for f, t in py._fields_]
         assert [f for f, _ in fields] == [f for f, _ in got], name
         assert [C.sizeof(t) for _, t in fields] == [C.sizeof(t) for _, t in got], name
-    assert C.sizeof(hrt.RtParams) == 19 * 4
+    assert C.sizeof(hrt.RtParams) == 17 * 4
     assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64 + 8 + 4 + 4 + 8
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(6)] == [80, 32, 48, 32, 64, C.sizeof(O.OParams)]

@@ -209,13 +209,16 @@ def _queue_render(sd, frames: int, **params):
     """Renders `sd` under the queue schedule with extra rt_params (fold, budget, slot cap, fault injection);
     returns (image, stats)."""
     r = scenes.make_renderer(sd)
+    faults = {k: params.pop(k) for k in ("ring_slots_max", "fail_alloc_above_mb") if k in params}
+    if faults:
+        r.set_faults(**faults)
     r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **params)
     r.draw_frames(frames, 1000, 10)
     return r.read_image(), r.stats()
 
 
 def test_fold_allocation_failure_shrinks_the_launches():
-    """Allocations the device refuses (fault injection, rt_params.fail_alloc_above_mb = 100: every colour-fold
+    """Allocations the device refuses (fault injection, rt_testing_set_faults(fail_alloc_above_mb = 100): every colour-fold
     allocation above 100 MiB fails): the sample buffer (512x512 x 100 frames = 315 MB) is halved until it fits
     (launches of 25 frames); with a 160 MiB budget (under 64 frames of colours) the fold ring (4096 slots x
     32 KB) halves its budget until it fits. Both bit-identical to the default draw."""
@@ -228,6 +231,43 @@ def test_fold_allocation_failure_shrinks_the_launches():
     assert st.launches == 2 and st.fold_bytes > 100 << 20
     np.testing.assert_array_equal(small.view(np.uint32), want.view(np.uint32))
     np.testing.assert_array_equal(ring.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("case", ["c3", "c4", "rows", "steal"])
+def test_band_pipeline_bit_identical(case):
+    """Sample-buffer draws whose colours exceed the budget run as pipelined BANDS (renderer.cpp launch_frames): launches
+    of tile-row bands x every frame on two side streams with two buffers of half the budget, each band's k_accumulate
+    on the renderer stream. Images and every work count equal the single-launch draw (32 GiB budget) and the oracle
+    on sampled rows; the colour memory stays within the budget; ragged last bands, a row partition (8-row blocks of
+    rank 1 of 3), stealing on short band launches and the triangle / mixed heap walk included."""
+    if case == "c3":
+        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {}, 1024          # 3 bands of 45 tile rows
+    elif case == "c4":
+        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 4}, 200   # 3 bands of 30 tile rows
+    elif case == "rows":
+        from hrt.parallel import rank_params
+        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 2}, 64
+    else:
+        sd, extra, budget = scenes.config_c3(960, 544, 16), {"job_frames": 1, "steal": 2}, 48
+    runs = []
+    for mb in (32768, budget):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb, **extra)
+        r.draw_frames(sd.frames, 1000, 10)
+        st = r.stats()
+        runs.append((r.read_image(), st))
+    (one, st1), (band, stb) = runs
+    assert st1.bands == 1 and stb.bands > 1 and stb.fold_ring == 0, (case, st1.bands, stb.bands, stb.fold_ring)
+    assert stb.launches == 2 * stb.bands and stb.trace_launches == stb.bands
+    assert stb.fold_bytes <= budget << 20, (case, stb.fold_bytes)
+    assert stb.device_bytes - stb.fold_bytes < st1.device_bytes  # the whole-draw buffer is gone
+    np.testing.assert_array_equal(one.view(np.uint32), band.view(np.uint32), err_msg=case)
+    assert (st1.queries, st1.node_tests, st1.tri_tests, st1.sphere_tests) == \
+        (stb.queries, stb.node_tests, stb.tri_tests, stb.sphere_tests), case
+    if case in ("c3", "c4"):  # every 97th row against the oracle
+        step = 97
+        ref, _ = scenes.oracle_render(sd, rows=(3, step, len(range(3, sd.height, step))))
+        assert_parity(band[3::step], ref, f"band pipeline {case}")
 
 
 def test_fold_memory_follows_the_budget():
@@ -303,7 +343,7 @@ def test_release_scratch_then_draw_again(budget_mb):
 
 @pytest.mark.parametrize("slots", [1, 2, 8])
 def test_fold_ring_slot_reuse_bit_identical(slots):
-    """Very few fold-ring slots (rt_params.ring_slots_max): nearly every job waits in the free queue for a slot
+    """Very few fold-ring slots (rt_testing_set_faults ring_slots_max): nearly every job waits in the free queue for a slot
     to be returned (1 slot: one job at a time). C3 (k_trace_split) and C4 (k_trace_split_tris) at 160x96,
     64 frames (two jobs per tile), and C2 (k_trace, four): images bit-identical to the tiles schedule, same
     ray counts."""
@@ -351,6 +391,46 @@ def test_row_partition_matches_full_image():
         r.draw_frames(6, 1000, 10)
         rows = owned_rows(row0, step, sd.height, block)
         np.testing.assert_array_equal(r.read_image().view(np.uint32), fimg[rows].view(np.uint32))
+
+
+def test_ranks_beyond_the_image_own_no_rows():
+    """with 8-row blocks dealt round-robin, a rank whose first block starts at or below the image's last
+    row owns no rows (20 rows over 4 ranks: rank 3 starts at row 24). Its renderer accepts the partition, its draws
+    trace nothing and its image is empty; the ranks' bands still reassemble to the full image. A resize that leaves
+    a renderer without rows keeps its partition (it used to reset row0 to 0 and render rank 0's rows), and growing
+    the image back gives it its blocks again."""
+    from hrt.parallel import assemble, max_rows, owned_rows, rank_params
+    import torch
+    sd = scenes.config_c3(48, 20, 4)
+    full = scenes.make_renderer(sd)
+    full.draw_frames(sd.frames, 1000, 10)
+    fimg = full.read_image()
+    world, parts, rays = 4, [], 0
+    for rank in range(world):
+        for sched in (hrt.RT_SCHEDULE_QUEUE, hrt.RT_SCHEDULE_TILES):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=sched, **rank_params(rank, world, 8))
+            r.draw_frames(sd.frames, 1000, 10)
+            img, st = r.read_image(), r.stats()
+            assert img.shape == (len(owned_rows(8 * rank, world, sd.height, 8)), sd.width, 3)
+            if rank == 3:
+                assert img.shape[0] == 0 and st.queries == 0 and st.local_rows == 0, (sched, st.queries)
+        rays += st.queries
+        band = np.zeros((max_rows(world, sd.height, 8), sd.width, 3), np.float32)
+        band[: len(img)] = img
+        parts.append(torch.from_numpy(band))
+    got = assemble(parts, sd.height, world, block=8).numpy()
+    np.testing.assert_array_equal(got.view(np.uint32), fimg.view(np.uint32))
+    assert rays == full.stats().queries
+    r = scenes.make_renderer(sd)
+    r.set_params(row0=8, row_step=2, row_block=8)
+    r.resize(sd.width, 8)  # rows 8.. are gone: no rows, partition kept
+    assert r.params.row0 == 8 and r.local_rows == 0
+    r.draw_frames(2, 1000, 10)
+    assert r.read_image().shape == (0, sd.width, 3) and r.stats().queries == 0
+    r.resize(sd.width, sd.height)
+    r.draw_frames(sd.frames, 1000, 10)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), fimg[owned_rows(8, 2, sd.height, 8)].view(np.uint32))
 
 
 @pytest.mark.parametrize("schedule", [0, 2])
@@ -519,10 +599,10 @@ def test_tail_split_bit_identical(jf):
 
 
 def test_heap_top_configs_bit_identical():
-    """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 eight levels with 256-lane workgroups, 3 nine levels
-    with 512, 4 almost ten with 768): the triangle program (Suzanne, the dragon with its capped walks), the mixed
-    program with the linear and the culling-BVH sphere scans; images and ray / node / triangle counts equal across
-    the configurations, with and without work stealing, and the oracle's."""
+    """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 on = nodes 1..991 with 768-lane workgroups, 0 auto =
+    on): the triangle program (Suzanne, the dragon with its capped walks), the mixed program with the linear and the
+    culling-BVH sphere scans; images and ray / node / triangle counts equal across the configurations, with and
+    without work stealing, and the oracle's. (The 8- and 9-level tops of round 3 were retired.)"""
     cases = [scenes.config_c4(120, 72, 5)]
     mixed = scenes.config_c4(96, 64, 4)
     mixed.spheres = np.concatenate([mixed.spheres] + [scenes.rtiow_spheres()[:60]])  # culling BVH sphere scan
@@ -532,14 +612,14 @@ def test_heap_top_configs_bit_identical():
         cases.append(scenes.SceneDef(builder, hrt.RT_MODE_TRIS, w, h, scene.camera, bvh=scene.tris_bvh.view(), frames=4))
     for sd in cases:
         runs = []
-        for heap_lds, steal in ((1, 1), (2, 1), (3, 1), (4, 1), (4, 2), (0, 0)):
+        for heap_lds, steal in ((1, 1), (2, 1), (1, 2), (2, 2), (0, 0)):
             r = scenes.make_renderer(sd)
             r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, heap_lds=heap_lds, steal=steal)
             r.draw_frames(sd.frames, 1000, 10)
             st = r.stats()
             runs.append((r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests), st.kernel.decode()))
         kernels = {k for _, _, k in runs}
-        assert len(kernels) >= 5, kernels  # every configuration ran its own instantiation
+        assert len(kernels) >= 4, kernels  # every configuration ran its own instantiation
         for img, counts, k in runs[1:]:
             np.testing.assert_array_equal(runs[0][0].view(np.uint32), img.view(np.uint32), err_msg=f"{sd.name} {k}")
             assert counts == runs[0][1], (sd.name, k, counts, runs[0][1])
@@ -702,9 +782,9 @@ def test_culling_bvh_with_zero_radius_slots():
 def test_split_walk_stack_overflow_falls_back_to_the_exact_scan():
     """2^17 coincident spheres: the culling BVH degenerates to 15 levels of median splits with every box
     hit, so k_trace_split's 14-entry LDS stack overflows and those queries fall back to the exact full
-    scan (more sphere tests than k_trace with its 24-entry stack). Every t ties, so the lowest slot must
-    win: slot 0 is the only lambertian among eight materials tiled over the slots. Both kernels give the
-    oracle's bits."""
+    scan (more sphere tests than the tiles kernel k_render with its 24-entry stack). Every t ties, so the lowest
+    slot must win: slot 0 is the only lambertian among eight materials tiled over the slots. Both kernels, and
+    k_trace_split with and without suspension, give the oracle's bits."""
     base = [hrt.Sphere.new_lambertian(hrt.Vec3(0.0, 0.0, -3.0), 1.0, hrt.Vec3(0.9, 0.3, 0.2))]
     base += [hrt.Sphere.new_metal(hrt.Vec3(0.0, 0.0, -3.0), 1.0, hrt.Vec3(0.1 * k, 0.8, 0.5), 0.05 * k)
              for k in range(1, 8)]
@@ -713,15 +793,18 @@ def test_split_walk_stack_overflow_falls_back_to_the_exact_scan():
     sd = scenes.SceneDef("coincident", hrt.RT_MODE_SPHERE, 24, 16, cam, sph, frames=2, bounces=8,
                          min_sphere_slots=0)
     runs = {}
-    for sb in (0, 24):
+    for key, params in (("tiles", {"schedule": hrt.RT_SCHEDULE_TILES}), (0, {"suspend_below": 0}),
+                        (24, {"suspend_below": 24})):
         r = scenes.make_renderer(sd)
-        r.set_params(variant=4, schedule=hrt.RT_SCHEDULE_QUEUE, suspend_below=sb)
+        r.set_params(variant=4, **({"schedule": hrt.RT_SCHEDULE_QUEUE} | params))
         r.draw_frames(sd.frames, 1000, 10)
-        runs[sb] = (r.read_image(), r.stats())
-    (img0, st0), (img1, st1) = runs[0], runs[24]
-    assert st0.suspend_below == 0 and st1.suspend_below == 24 and st1.queries == st0.queries
-    assert st1.sphere_tests > st0.sphere_tests, (st1.sphere_tests, st0.sphere_tests)  # the fallback ran
+        runs[key] = (r.read_image(), r.stats())
+    (img0, st0), (img1, st1), (imgt, stt) = runs[0], runs[24], runs["tiles"]
+    assert st0.suspend_below == 0 and st1.suspend_below == 24 and st1.queries == st0.queries == stt.queries
+    assert st1.sphere_tests == st0.sphere_tests  # same walk, suspended or not
+    assert st1.sphere_tests > stt.sphere_tests, (st1.sphere_tests, stt.sphere_tests)  # the fallback ran
     np.testing.assert_array_equal(img0.view(np.uint32), img1.view(np.uint32))
+    np.testing.assert_array_equal(imgt.view(np.uint32), img1.view(np.uint32))
     ref, q = scenes.oracle_render(sd)
     assert q == st1.queries
     assert_parity(img1, ref, "coincident spheres, stack overflow")
