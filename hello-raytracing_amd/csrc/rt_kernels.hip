@@ -394,7 +394,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             } else {
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
-                    if (sp < STACK) {
+                    if (NOOVF || sp < STACK) {
                         stack[sp * LS] = lfirst ? right : left;
                         sp++;
                     } else {

@@ -236,17 +236,17 @@ def test_fold_allocation_failure_shrinks_the_launches():
 @pytest.mark.parametrize("case", ["c3", "c4", "rows", "steal"])
 def test_band_pipeline_bit_identical(case):
     """Sample-buffer draws whose colours exceed the budget run as pipelined BANDS (renderer.cpp launch_frames): launches
-    of tile-row bands x every frame on two side streams with two buffers of half the budget, each band's k_accumulate
+    of tile-row bands x every frame on two side streams with three buffers of a third of the budget, each band's k_accumulate
     on the renderer stream. Images and every work count equal the single-launch draw (32 GiB budget) and the oracle
     on sampled rows; the colour memory stays within the budget; ragged last bands, a row partition (8-row blocks of
     rank 1 of 3), stealing on short band launches and the triangle / mixed heap walk included."""
     if case == "c3":
-        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {}, 1024          # 3 bands of 45 tile rows
+        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {}, 1400          # 4 bands of 34 tile rows
     elif case == "c4":
-        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 4}, 200   # 3 bands of 30 tile rows
+        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 4}, 200   # 4 bands of 23 tile rows
     elif case == "rows":
         from hrt.parallel import rank_params
-        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 2}, 64
+        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 1}, 64
     else:
         sd, extra, budget = scenes.config_c3(960, 544, 16), {"job_frames": 1, "steal": 2}, 48
     runs = []
