@@ -149,10 +149,10 @@ struct rt_renderer {
     uint32_t time = 0, frame_count = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    // pipelined band launches of the sample buffer (launch_frames): band i traces on side[i % 2], its k_accumulate
-    // runs on `stream`; fork / trace-done / accumulate-done events (no timing)
+    // pipelined band launches of the sample buffer (launch_frames): band i traces on side[i % 2] and folds band
+    // i - 2 in its drain; fork / join events (no timing)
     hipStream_t side[2] = {nullptr, nullptr};
-    hipEvent_t ev_fork = nullptr, ev_tdone[2] = {nullptr, nullptr}, ev_adone[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_tdone[2] = {nullptr, nullptr};
 
     DevBuf<float> image;
     DevBuf<float4> sph_geo;
@@ -178,7 +178,7 @@ struct rt_renderer {
     DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
     uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
-    DevBuf<float> samples2, samples3;  // the other band buffers of the pipelined band launches (launch_frames)
+    DevBuf<float> band_buf[3];  // the other sample buffers of the pipelined band launches (launch_frames)
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
@@ -207,7 +207,7 @@ struct rt_renderer {
     uint64_t device_bytes() const {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
-               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + samples2.bytes() + samples3.bytes() + ring.bytes() + ring_ctl.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + band_buf[0].bytes() + band_buf[1].bytes() + band_buf[2].bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
@@ -556,13 +556,15 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a
         // launch, then k_accumulate) or the bounded-memory fold ring. With the sample buffer a launch covers
         //   1. the whole draw (every row, every frame) when its colours fit the budget: one buffer;
-        //   2. else, when one tile row x every frame fits a third of the budget, a BAND of tile rows x every frame:
-        //      the bands run as pipelined launches on two side streams with three buffers — band i + 1's trace fills
-        //      the CUs band i's drain leaves idle, band i's k_accumulate (on the renderer stream) runs in a later
-        //      drain, and band i + 3 reuses band i's buffer once that fold is done (with two buffers band i + 2 waited
-        //      for a fold that only gets CUs in band i + 1's drain) — so the colour memory is bounded by the budget while
-        //      every tile still has all its frames (and jobs) in one launch, the coherence a launch of fewer frames
-        //      loses (C3 at 82 / 164 / 344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1);
+        //   2. else, when one tile row x every frame fits a quarter of the budget, a BAND of tile rows x every frame:
+        //      the bands run as pipelined launches on two side streams with four buffers — band i + 1's trace fills
+        //      the CUs band i's drain leaves idle, band i's waves fold band i - 2 (same stream: complete) in that drain
+        //      (rt_kernels.hip drain_fold), and band i + 2 reuses band i - 2's buffer in stream order; the last two
+        //      bands get a k_accumulate each. So the colour memory is bounded by the budget while every tile still has
+        //      all its frames (and jobs) in one launch, the coherence a launch of fewer frames loses (C3 at 82 / 164 /
+        //      344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1). (A k_accumulate per band on the
+        //      renderer stream, three buffers, measured C3 -3 %: the fold got few CUs beside the persistent traces and
+        //      held the buffer band i + 3 waited for; profiles/r04/band/timeline_c3_8g.txt);
         //   3. else frame chunks of the whole image, as many frames as the budget holds; the fold ring (auto) when that
         //      is under min(count, 320) frames.
         size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
@@ -572,11 +574,14 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         uint32_t chunk = std::max(count, 1u), bt = P.tiles_h, log2s = 0;
         bool bands = false;
         // (a band launch needs jobs for the persistent grid: at least 64 per CU — 16 Ki on MI355X, 2.3 per resident wave
-        // of k_trace_split; a band of a third of an 8 GiB budget holds 116 Ki 32-frame jobs whatever the frame count)
+        // of k_trace_split; a band of a quarter of an 8 GiB budget holds 87 Ki 32-frame jobs whatever the frame count)
         const uint64_t band_jobs_min = 64ull * std::max(r->cus, 1u);
-        constexpr uint32_t NBUF = 3;  // band buffers in flight
+        constexpr uint32_t NBUF = 4;  // band buffers in flight
         const uint32_t bt_fit = (uint32_t)std::min<size_t>(P.tiles_h, (budget / NBUF) / (row_floats * 4u * chunk));
-        if (r->params.fold != RT_FOLD_RING && frame_floats * 4u * chunk > budget && bt_fit >= 1u &&
+#ifndef HRT_BANDS
+#define HRT_BANDS 1
+#endif
+        if (HRT_BANDS && r->params.fold != RT_FOLD_RING && frame_floats * 4u * chunk > budget && bt_fit >= 1u &&
             (uint64_t)bt_fit * P.tiles_w * ((chunk + jf - 1u) / jf) >= band_jobs_min) {
             bands = true;
             const uint32_t nb = (P.tiles_h + bt_fit - 1u) / bt_fit;
@@ -597,12 +602,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 const size_t need = (size_t)bt * chunk * row_floats;
                 const size_t cap = std::max(bands ? budget / NBUF : budget, need * 4u);
                 rc = ensure_within(r->samples, need, cap, fail_above);
-                if (!rc && bands) rc = ensure_within(r->samples2, need, cap, fail_above);
-                if (!rc && bands) rc = ensure_within(r->samples3, need, cap, fail_above);
+                for (DevBuf<float>& b : r->band_buf)
+                    if (!rc && bands) rc = ensure_within(b, need, cap, fail_above);
                 if (rc != RT_ERR_ALLOC) break;
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
-                r->samples2.release();
-                r->samples3.release();
+                for (DevBuf<float>& b : r->band_buf) b.release();
                 if (bands && bt > 1u) {
                     bt = (bt + 1u) / 2u;
                 } else if (chunk > 1u) {
@@ -612,16 +616,13 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 }
             }
             if (rc) return rc;
-            if (!bands) {
-                r->samples2.release();
-                r->samples3.release();
-            }
+            if (!bands)
+                for (DevBuf<float>& b : r->band_buf) b.release();
             r->ring_slots = 0;
             r->fold_bytes = (uint64_t)(bands ? NBUF : 1u) * bt * chunk * row_floats * 4u;
         } else {
             r->samples.release();
-            r->samples2.release();
-            r->samples3.release();
+            for (DevBuf<float>& b : r->band_buf) b.release();
             // frames per launch: at most FOLD_MAX_JOBS jobs per tile (the done bits of the tile's fold word)
             chunk = std::max(1u, std::min(count, hrt_dev::FOLD_MAX_JOBS * jf));
             const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
@@ -677,19 +678,36 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             HIP_TRY(hipEventRecord(r->ev_fork, r->stream));
             for (hipStream_t sst : r->side) HIP_TRY(hipStreamWaitEvent(sst, r->ev_fork, 0));
         }
+        // the drain fold needs every frame in one launch per band (each tile's frames folded by one launch); a band
+        // plan cut to frame chunks by a short device (the allocation loop above), and the opt-in SAH walk (k_trace<..,
+        // true> has no drain fold), run their bands on one stream, each folded by a k_accumulate right after it
+        const bool dfold = bands && chunk >= count && !P.tri_bvh;
+        float* const bufs[NBUF] = {r->samples.ptr, r->band_buf[0].ptr, r->band_buf[1].ptr, r->band_buf[2].ptr};
         uint32_t li = 0;  // launch index
         for (uint32_t done = 0; done < count; done += chunk) {
             for (uint32_t band = 0; band < nbands; band++, li++) {
-                const uint32_t k = bands ? (li & 1u) : 0u;   // side stream of this launch
+                const uint32_t k = dfold ? (li & 1u) : 0u;   // side stream of this launch
                 const uint32_t kb = bands ? li % NBUF : 0u;  // and its buffer
                 P.kr0 = band * bt * 8u;
                 P.nrows = bands ? std::min(bt * 8u, nrows_all - P.kr0) : nrows_all;
                 P.tiles_h = bands ? (P.nrows + 7u) / 8u : th_all;
                 P.image = image0 + (size_t)P.kr0 * r->width * 3u;
-                float* const bufs[NBUF] = {r->samples.ptr, r->samples2.ptr, r->samples3.ptr};
                 P.samples = P.ring_mode ? nullptr : bufs[kb];
                 P.queue = r->counter.ptr + (k ? hrt_dev::QUEUE2 : 15u);
                 P.steal_slots = r->steal_slots.ptr + (size_t)k * P.steal_cap;
+                // band li - 2 (this stream's previous launch: complete when this one starts) is folded in this drain
+                P.dfold_samples = nullptr;
+                P.dfold_image = nullptr;
+                P.dfold_next = nullptr;
+                P.dfold_tiles = P.dfold_nrows = 0u;
+                if (dfold && band >= 2u) {
+                    const uint32_t pkr0 = (band - 2u) * bt * 8u;
+                    P.dfold_samples = bufs[(li - 2u) % NBUF];
+                    P.dfold_image = image0 + (size_t)pkr0 * r->width * 3u;
+                    P.dfold_nrows = std::min(bt * 8u, nrows_all - pkr0);
+                    P.dfold_tiles = P.tiles_w * ((P.dfold_nrows + 7u) / 8u);
+                    P.dfold_next = r->counter.ptr + hrt_dev::DFOLD + k;
+                }
                 P.nframes = std::min(chunk, count - done);
                 P.time0 = time0 + done * dtime;
                 P.frame0 = r->frame_count + done;
@@ -699,11 +717,12 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 // Auto stealing: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job
                 // dealt late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for
                 // long launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 ->
-                // 0.88)
+                // 0.88), and for pipelined bands but the last, whose drains the next band fills
                 {
                     const bool fits = lt < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
+                    const bool covered = dfold && band + 1u < nbands;
                     const bool want = r->params.steal == 2u ||
-                                      (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
+                                      (r->params.steal == 0u && !covered && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
                     P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
                 }
                 // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
@@ -719,8 +738,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 }
                 r->ring_nchunks = P.nchunks;
                 hipStream_t st = bands ? r->side[k] : r->stream;
-                if (bands && li >= NBUF) HIP_TRY(hipStreamWaitEvent(st, r->ev_adone[kb], 0));  // buffer kb folded
                 HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), st));
+                if (P.dfold_next) HIP_TRY(hipMemsetAsync(P.dfold_next, 0, sizeof(unsigned long long), st));
                 if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), st));
                 if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), st));
                 rc = trace_events(r, r->trace_pairs_pending);
@@ -730,17 +749,23 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], st));
                 r->trace_pairs_pending++;
                 launches++;
-                if (bands) {
-                    HIP_TRY(hipEventRecord(r->ev_tdone[k], st));
-                    HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_tdone[k], 0));
-                }
-                if (!P.ring_mode) {
-                    HIP_TRY(hrt_launch_accumulate(P, r->stream));
+                // the sample buffer of a launch no later band folds in its drain: k_accumulate after it, same stream
+                if (!P.ring_mode && (!dfold || band + 2u >= nbands)) {
+                    HIP_TRY(hrt_launch_accumulate(P, st));
                     launches++;
-                    if (bands) HIP_TRY(hipEventRecord(r->ev_adone[kb], r->stream));
                 }
             }
         }
+        if (bands) {  // the renderer stream (ev_stop, readback) waits for both side streams
+            for (uint32_t k = 0; k < 2u; k++) {
+                HIP_TRY(hipEventRecord(r->ev_tdone[k], r->side[k]));
+                HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_tdone[k], 0));
+            }
+        }
+        P.dfold_samples = nullptr;
+        P.dfold_image = nullptr;
+        P.dfold_next = nullptr;
+        P.dfold_tiles = P.dfold_nrows = 0u;
         P.kr0 = 0u;
         P.nrows = nrows_all;
         P.tiles_h = th_all;
@@ -854,8 +879,7 @@ void delete_buffers(rt_renderer* r) {
     r->counter.release();
     r->steal_slots.release();
     r->samples.release();
-    r->samples2.release();
-    r->samples3.release();
+    for (DevBuf<float>& b : r->band_buf) b.release();
     r->ring.release();
     r->ring_ctl.release();
     r->wave_trace.release();
@@ -922,7 +946,6 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     for (int k = 0; k < 2 && ok; k++)
         ok = hipStreamCreateWithFlags(&r->side[k], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&r->ev_tdone[k], hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; k < 3 && ok; k++) ok = hipEventCreateWithFlags(&r->ev_adone[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         rt_destroy(r);
         return fail(RT_ERR_DEVICE, "rt_create: stream/event creation failed");
@@ -947,8 +970,6 @@ int rt_destroy(rt_renderer* r) {
     if (r->ev_start) (void)hipEventDestroy(r->ev_start);
     if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
     if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
-    for (int k = 0; k < 3; k++)
-        if (r->ev_adone[k]) (void)hipEventDestroy(r->ev_adone[k]);
     for (int k = 0; k < 2; k++) {
         if (r->ev_tdone[k]) (void)hipEventDestroy(r->ev_tdone[k]);
         if (r->side[k]) (void)hipStreamDestroy(r->side[k]);
@@ -1189,8 +1210,7 @@ int rt_release_scratch(rt_renderer* r) {
     }
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->samples.release();
-    r->samples2.release();
-    r->samples3.release();
+    for (DevBuf<float>& b : r->band_buf) b.release();
     r->ring.release();
     r->ring_ctl.release();
     return RT_OK;

@@ -79,8 +79,9 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 // (renderer.cpp decides, the kernel bounds its copy by the same constant).
 // device counter words: [0, 16) exported (include/hrt.h RT_RAW_COUNTERS; [15] = the job queue of the first
 // stream), then the fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue
-// overruns; [20] the job queue of the second stream (pipelined band launches, renderer.cpp)
-constexpr uint32_t WATCHDOG = 16, QUEUE2 = 20, COUNTER_WORDS = 21;
+// overruns; [20] the job queue of the second stream (pipelined band launches, renderer.cpp), [21, 23) the drain
+// fold's tile claims of the two streams
+constexpr uint32_t WATCHDOG = 16, QUEUE2 = 20, DFOLD = 21, COUNTER_WORDS = 23;
 
 // fold ring: jobs per tile and launch (the done bits of a tile's fold word, rt_kernels.hip)
 constexpr uint32_t FOLD_MAX_JOBS = 48;
@@ -172,6 +173,13 @@ struct KParams {
     unsigned long long* steal_slots;  // one per wave: (job + 1) << 32 | frames claimed; zeroed per launch
     uint32_t steal, nwaves;       // on; waves of the launch (launch_persistent)
     uint32_t steal_cap, pad_s;    // slots allocated (bounds the grid)
+    // drain fold (pipelined bands, renderer.cpp): once its jobs are done, each wave of a band launch folds tiles of
+    // the band launched two before it on the same stream (complete by stream order) into the image before it
+    // exits — the fold runs in this launch's drain, not in a k_accumulate that competes with the next band's waves
+    const float* dfold_samples;   // that band's sample buffer; nullptr: no drain fold
+    float* dfold_image;           // its first image row
+    unsigned long long* dfold_next;  // tile claims (zeroed per launch)
+    uint32_t dfold_tiles, dfold_nrows;  // its tiles (tiles_w x its tile rows) and rows; frames as this launch's
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

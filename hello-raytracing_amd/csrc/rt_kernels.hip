@@ -1145,6 +1145,67 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
     __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(), (int)off, 0, 16 /* sc1: write-through */);
 }
 
+// Folds the sample buffer's colours of one tile's pixels into the image in frame order with the mix k_render uses
+// (WGSL mix, shader_sphere.wgsl:264-271) — k_accumulate and the bands' drain fold. `tile` (wave-uniform) points at the
+// tile's frame 0, frame f at tile + f * fstride; the lane's pixel is 3 floats at lane3. U frames' loads are issued
+// before their mixes (a wave's frame is 768 B: one load in flight per wave left k_accumulate latency-bound); the
+// uniform frame address + a 32-bit lane offset keeps each load to one VGPR of address (global_load saddr).
+template <int U>
+__device__ __forceinline__ void fold_pixel(float* px, const float* tile, uint32_t lane3, size_t fstride, uint32_t nframes,
+                                           uint32_t frame0, float ema_cap) {
+    float acc0 = px[0], acc1 = px[1], acc2 = px[2];
+    uint32_t f = 0;
+    for (; f + (uint32_t)U <= nframes; f += (uint32_t)U, tile += (size_t)U * fstride) {
+        float v[U][3];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const float* fr = tile + (size_t)j * fstride;
+            v[j][0] = fr[lane3];
+            v[j][1] = fr[lane3 + 1u];
+            v[j][2] = fr[lane3 + 2u];
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const float w = 1.0f / (fmin_ieee((float)(frame0 + f + (uint32_t)j), ema_cap) + 1.0f);
+            const float omw = 1.0f - w;
+            acc0 = acc0 * omw + (0.0f + v[j][0]) * w;
+            acc1 = acc1 * omw + (0.0f + v[j][1]) * w;
+            acc2 = acc2 * omw + (0.0f + v[j][2]) * w;
+        }
+    }
+    for (; f < nframes; f++, tile += fstride) {
+        const float w = 1.0f / (fmin_ieee((float)(frame0 + f), ema_cap) + 1.0f);
+        const float omw = 1.0f - w;
+        acc0 = acc0 * omw + (0.0f + tile[lane3]) * w;
+        acc1 = acc1 * omw + (0.0f + tile[lane3 + 1u]) * w;
+        acc2 = acc2 * omw + (0.0f + tile[lane3 + 2u]) * w;
+    }
+    px[0] = acc0;
+    px[1] = acc1;
+    px[2] = acc2;
+}
+
+// The drain fold of a band launch (KParams dfold_*): after its own jobs, the wave claims whole tiles of the earlier
+// band (one pixel per lane, every frame in order) until none is left. Reached by every wave of the launch (after its
+// job loop), so each claimed tile is folded exactly once before the launch ends.
+template <int U = 4>
+__device__ __forceinline__ void drain_fold(uint32_t lane) {
+    const KPtr K = kargs();
+    if (K->dfold_samples == nullptr) return;
+    const uint32_t ntiles = K->dfold_tiles, tw = K->tiles_w;
+    const size_t fstride = (size_t)ntiles * 64u * 3u;
+    while (true) {
+        uint32_t t = 0;
+        if (lane == 0) t = (uint32_t)min(atomicAdd(K->dfold_next, 1ull), 0xFFFFFFFFull);
+        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0));  // (every lane holds lane 0's claim)
+        if (t >= ntiles) break;
+        const uint32_t x = (t % tw) * 8u + (lane & 7u), kr = (t / tw) * 8u + (lane >> 3);
+        if (x < K->W && kr < K->dfold_nrows)
+            fold_pixel<U>(K->dfold_image + ((size_t)kr * K->W + x) * 3u, K->dfold_samples + (size_t)t * 192u, lane * 3u,
+                          fstride, K->nframes, K->frame0, K->ema_cap);
+    }
+}
+
 #ifdef HRT_RINGSTAT
 // diagnostic build: per-wave ring statistics (stall rounds: every entry busy; slot-wait rounds; folds; fold
 // cycles / 16), summed into counter[5..8] at wave exit
@@ -1827,6 +1888,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #endif
         job_account(J, fin, fl, lane);
     }
+    // (not in the SAH-walk instantiations, where the fold's code cost a wave per SIMD: renderer.cpp folds their
+    // bands with k_accumulate)
+    if constexpr (!TSAH) drain_fold<2>(lane);
 #ifdef HRT_STAMPS
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
@@ -2158,6 +2222,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_PHASE(3);
     }
     HRT_PHASE_FLUSH
+    drain_fold(lane);
 #if defined(HRT_STAMPS) && !defined(HRT_PHASES)
     {
         unsigned long long v[7] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
@@ -2316,6 +2381,7 @@ k_trace_split_tris(const KParams P) {
         HRT_PHASE(3);
     }
     HRT_PHASE_FLUSH
+    drain_fold(lane);
 #ifdef HRT_RINGSTAT
     if (lane == 0)
         for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
@@ -2344,19 +2410,9 @@ __global__ __launch_bounds__(256) void k_accumulate(const KParams P) {
     const uint32_t x = (tile % P.tiles_w) * 8u + (l & 7u);
     const uint32_t kr = (tile / P.tiles_w) * 8u + (l >> 3);
     if (x >= P.W || kr >= P.nrows) return;
-    float* px = P.image + ((size_t)kr * P.W + x) * 3u;
-    float acc0 = px[0], acc1 = px[1], acc2 = px[2];
-    const float* c = P.samples + q * 3u;
-    for (uint32_t f = 0; f < P.nframes; f++, c += npad * 3u) {
-        const float w = 1.0f / (fmin_ieee((float)(P.frame0 + f), P.ema_cap) + 1.0f);
-        const float omw = 1.0f - w;
-        acc0 = acc0 * omw + (0.0f + c[0]) * w;
-        acc1 = acc1 * omw + (0.0f + c[1]) * w;
-        acc2 = acc2 * omw + (0.0f + c[2]) * w;
-    }
-    px[0] = acc0;
-    px[1] = acc1;
-    px[2] = acc2;
+    const uint32_t wtile = __builtin_amdgcn_readfirstlane(tile);  // (a wave is one tile)
+    fold_pixel<8>(P.image + ((size_t)kr * P.W + x) * 3u, P.samples + (size_t)wtile * 192u, l * 3u, npad * 3u, P.nframes,
+                  P.frame0, P.ema_cap);
 }
 
 hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {

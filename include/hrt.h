@@ -71,11 +71,12 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; default 8192. The sample buffer: one launch
-                                  when a draw's colours fit; else bands of tile rows x every frame in two
-                                  buffers of half the budget, pipelined over two streams; else launches of
-                                  as many frames as fit, or the fold ring below min(frames, 320) frames
-                                  (bounded memory, slower)                                 */
+    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; default 32768. The sample buffer: one
+                                  launch when a draw's colours fit; else bands of tile rows x every frame in
+                                  four buffers of a quarter of the budget, pipelined over two streams (each
+                                  band folds the band two before it in its drain); else launches of as many
+                                  frames as fit, or the fold ring below min(frames, 320) frames (bounded
+                                  memory, slower)                                          */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
                                   power of two (at most 1024); default 0 = per kernel: 32 with the
                                   suspendable walks, 16 for the linear sphere scans                      */
@@ -196,7 +197,7 @@ int rt_synchronize(rt_renderer *r);
 int rt_get_stats(const rt_renderer *r, rt_stats *out);
 /* Frees the sample queue's colour-fold memory (the sample buffer or the fold ring, rt_stats.fold_bytes)
  * after the pending draws; the next queue draw allocates it again. For a renderer kept alive between
- * renders beside other work: the default 8 GiB budget lets one C3 render hold 7.6 GB (no reference
+ * renders beside other work: one C3 render holds 7.6 GB under the default budget (no reference
  * counterpart: wgpu frees nothing either, but the reference has no per-sample buffer). */
 int rt_release_scratch(rt_renderer *r);
 

@@ -233,32 +233,42 @@ def test_fold_allocation_failure_shrinks_the_launches():
     np.testing.assert_array_equal(ring.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("case", ["c3", "c4", "rows", "steal"])
+@pytest.mark.parametrize("case", ["c3", "c4", "rows", "steal", "chunked"])
 def test_band_pipeline_bit_identical(case):
     """Sample-buffer draws whose colours exceed the budget run as pipelined BANDS (renderer.cpp launch_frames): launches
-    of tile-row bands x every frame on two side streams with three buffers of a third of the budget, each band's k_accumulate
-    on the renderer stream. Images and every work count equal the single-launch draw (32 GiB budget) and the oracle
-    on sampled rows; the colour memory stays within the budget; ragged last bands, a row partition (8-row blocks of
-    rank 1 of 3), stealing on short band launches and the triangle / mixed heap walk included."""
+    of tile-row bands x every frame on two side streams with four buffers of a quarter of the budget; band i's waves
+    fold band i - 2 in their drain (rt_kernels.hip drain_fold), the last two bands get a k_accumulate. Images and every
+    work count equal the single-launch draw (32 GiB budget) and the oracle on sampled rows; the colour memory stays
+    within the budget; ragged last bands, a row partition (8-row blocks of rank 1 of 3), stealing on short band
+    launches, the triangle / mixed heap walk, and a device too short for one tile row x every frame (fault injection:
+    frame chunks of bands on one stream, a k_accumulate after each) included."""
+    fault = {}
     if case == "c3":
-        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {}, 1400          # 4 bands of 34 tile rows
+        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {"job_frames": 16}, 1100  # 6 bands: 5 x 23 + 20 tile rows
     elif case == "c4":
-        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 4}, 200   # 4 bands of 23 tile rows
-    elif case == "rows":
+        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 2}, 150   # 7 bands: 6 x 13 + 12
+    elif case in ("rows", "chunked"):
         from hrt.parallel import rank_params
-        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 1}, 64
+        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 1}, 64  # 8: 7 x 4 + 2
+        if case == "chunked":  # one tile row x 32 frames is 3.9 MB: bands of one tile row x 16 frames
+            fault = {"fail_alloc_above_mb": 2}
     else:
-        sd, extra, budget = scenes.config_c3(960, 544, 16), {"job_frames": 1, "steal": 2}, 48
+        sd, extra, budget = scenes.config_c3(960, 544, 16), {"job_frames": 1, "steal": 2}, 56  # 8: 7 x 9 + 5
     runs = []
     for mb in (32768, budget):
         r = scenes.make_renderer(sd)
+        if mb == budget and fault:
+            r.set_faults(**fault)
         r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb, **extra)
         r.draw_frames(sd.frames, 1000, 10)
         st = r.stats()
         runs.append((r.read_image(), st))
     (one, st1), (band, stb) = runs
     assert st1.bands == 1 and stb.bands > 1 and stb.fold_ring == 0, (case, st1.bands, stb.bands, stb.fold_ring)
-    assert stb.launches == 2 * stb.bands and stb.trace_launches == stb.bands
+    if case == "chunked":
+        assert stb.bands == 30 and stb.trace_launches == 2 * stb.bands and stb.launches == 2 * stb.trace_launches, stb
+    else:
+        assert stb.trace_launches == stb.bands and stb.launches == stb.bands + 2, (case, stb.launches, stb.bands)
     assert stb.fold_bytes <= budget << 20, (case, stb.fold_bytes)
     assert stb.device_bytes - stb.fold_bytes < st1.device_bytes  # the whole-draw buffer is gone
     np.testing.assert_array_equal(one.view(np.uint32), band.view(np.uint32), err_msg=case)
