@@ -568,8 +568,8 @@ def main() -> int:
                 # "sample-buffer" (+ k_accumulate) or the bounded-memory "fold-ring"; device bytes it used
                 "fold": ("fold-ring" if st_last.fold_ring else "sample-buffer") if schedule == 2 else "in-register",
                 "fold_bytes": int(st_last.fold_bytes) if schedule == 2 else 0,
-                # sample buffer: row bands of the draw's pipelined launches (1 = one launch covers every row)
-                "bands": int(st_last.bands) if schedule == 2 else 0,
+                # frames per trace launch (the sample buffer's balanced launches, rt_params.queue_budget_mb)
+                "launch_frames": int(st_last.launch_frames) if schedule == 2 else 0,
             },
             # The path is FP32-VALU issue bound (no MFMA: no dense contraction; HBM ~2 % busy). `achieved` =
             # the FP32 FLOPs the kernel executes (its exact in-kernel test counters x FLOP per test, + the

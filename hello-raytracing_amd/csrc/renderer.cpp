@@ -149,10 +149,6 @@ struct rt_renderer {
     uint32_t time = 0, frame_count = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    // pipelined band launches of the sample buffer (launch_frames): band i traces on side[i % 2] and folds band
-    // i - 2 in its drain; fork / join events (no timing)
-    hipStream_t side[2] = {nullptr, nullptr};
-    hipEvent_t ev_fork = nullptr, ev_tdone[2] = {nullptr, nullptr};
 
     DevBuf<float> image;
     DevBuf<float4> sph_geo;
@@ -178,7 +174,6 @@ struct rt_renderer {
     DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
     uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
-    DevBuf<float> band_buf[3];  // the other sample buffers of the pipelined band launches (launch_frames)
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
@@ -197,17 +192,17 @@ struct rt_renderer {
     uint32_t last_suspend = 0;
     uint32_t test_ring_slots_max = 0, test_fail_alloc_above_mb = 0;  // hrt_testing.h fault injection
     uint32_t ring_slots = 0;  // fold-ring slots of the last sample-queue draw
-    uint32_t stats_bands = 0; // row bands of the last sample-queue draw's launches (1: one launch covers every row)
     uint32_t ring_tiles = 0, ring_nchunks = 0;  // (diagnostics: HRT_RING_DUMP)
     size_t ring_ctl_words = 0;
     uint64_t fold_bytes = 0;  // device memory of the last sample-queue draw's colour fold (rt_stats.fold_bytes)
+    uint32_t last_launch_frames = 0;  // frames per trace launch of the last sample-queue draw (rt_stats.launch_frames)
     unsigned long long raw_counters[RT_RAW_COUNTERS] = {};
 
     uint32_t row_block() const { return std::max(params.row_block, 1u); }
     uint64_t device_bytes() const {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
-               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + band_buf[0].bytes() + band_buf[1].bytes() + band_buf[2].bytes() + ring.bytes() + ring_ctl.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
@@ -553,76 +548,54 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         P.jf_log2 = 0;
         while ((2u << P.jf_log2) <= std::min(jf, 1024u)) P.jf_log2++;
         jf = 1u << P.jf_log2;
-        // How the colours are folded (rt_params.queue_budget_mb): the sample buffer (every colour of a
-        // launch, then k_accumulate) or the bounded-memory fold ring. With the sample buffer a launch covers
-        //   1. the whole draw (every row, every frame) when its colours fit the budget: one buffer;
-        //   2. else, when one tile row x every frame fits a quarter of the budget, a BAND of tile rows x every frame:
-        //      the bands run as pipelined launches on two side streams with four buffers — band i + 1's trace fills
-        //      the CUs band i's drain leaves idle, band i's waves fold band i - 2 (same stream: complete) in that drain
-        //      (rt_kernels.hip drain_fold), and band i + 2 reuses band i - 2's buffer in stream order; the last two
-        //      bands get a k_accumulate each. So the colour memory is bounded by the budget while every tile still has
-        //      all its frames (and jobs) in one launch, the coherence a launch of fewer frames loses (C3 at 82 / 164 /
-        //      344 frames per launch 29.3 / 31.5 / 32.4 Grays/s, C4 5.1 / 7.3 / 8.1). (A k_accumulate per band on the
-        //      renderer stream, three buffers, measured C3 -3 %: the fold got few CUs beside the persistent traces and
-        //      held the buffer band i + 3 waited for; profiles/r04/band/timeline_c3_8g.txt);
-        //   3. else frame chunks of the whole image, as many frames as the budget holds; the fold ring (auto) when that
-        //      is under min(count, 320) frames.
-        size_t budget = (size_t)std::max<uint32_t>(r->params.queue_budget_mb, 1u) << 20;
-        const size_t row_floats = (size_t)P.tiles_w * 64u * 3u;      // one tile row x one frame (tile-padded)
-        const size_t frame_floats = row_floats * P.tiles_h;
-        const size_t fail_above = (size_t)r->test_fail_alloc_above_mb << 20;
-        uint32_t chunk = std::max(count, 1u), bt = P.tiles_h, log2s = 0;
-        bool bands = false;
-        // (a band launch needs jobs for the persistent grid: at least 64 per CU — 16 Ki on MI355X, 2.3 per resident wave
-        // of k_trace_split; a band of a quarter of an 8 GiB budget holds 87 Ki 32-frame jobs whatever the frame count)
-        const uint64_t band_jobs_min = 64ull * std::max(r->cus, 1u);
-        constexpr uint32_t NBUF = 4;  // band buffers in flight
-        const uint32_t bt_fit = (uint32_t)std::min<size_t>(P.tiles_h, (budget / NBUF) / (row_floats * 4u * chunk));
-#ifndef HRT_BANDS
-#define HRT_BANDS 1
-#endif
-        if (HRT_BANDS && r->params.fold != RT_FOLD_RING && frame_floats * 4u * chunk > budget && bt_fit >= 1u &&
-            (uint64_t)bt_fit * P.tiles_w * ((chunk + jf - 1u) / jf) >= band_jobs_min) {
-            bands = true;
-            const uint32_t nb = (P.tiles_h + bt_fit - 1u) / bt_fit;
-            bt = (P.tiles_h + nb - 1u) / nb;  // balanced bands
-        } else if (frame_floats * 4u * chunk > budget) {
-            chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, budget / (frame_floats * 4u)));
+        // How the colours are folded (rt_params.queue_budget_mb, fold): the sample buffer (every colour
+        // of a launch, then k_accumulate) in launches of equal frame counts, or the bounded-memory fold ring.
+        //   queue_budget_mb 0 (auto, the default): floor(count / 320) launches (at least one). A launch of 320+ frames
+        //     loses ~2 % to one launch of every frame (C3 3 x 342 frames: 33.8 vs 34.5 Grays/s), shorter ones lose more
+        //     (fewer jobs per tile spread the waves over more of the image; C3 at 82 / 164 frames 29.3 / 31.5, C4 in
+        //     launches of 345 + 167 frames -13 %), so the buffer holds at most 639 frames (C3: 8.5 GB, not 25.5), and at
+        //     most AUTO_BUDGET;
+        //   queue_budget_mb > 0: a cap in MiB, launches of as many frames as it holds, balanced;
+        //   the fold ring (fold 0) when a launch would get fewer than min(count, 320) frames.
+        // (Pipelined launches of tile-row bands x every frame, which keep every frame of a tile in one launch within a
+        // bounded buffer, measured bit-identical but slower than these launches at the same budget: C3 tie, C4 -13 %,
+        // C5 -19 %; profiles/r04/band/.)
+        constexpr size_t AUTO_BUDGET = 32768ull << 20;
+        const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
+        const size_t frame_bytes = frame_floats * 4u;
+        const uint32_t nframes_all = std::max(count, 1u);
+        size_t budget = (size_t)r->params.queue_budget_mb << 20;
+        if (r->params.queue_budget_mb == 0u) {
+            const uint32_t n = std::max(1u, nframes_all / 320u);
+            budget = std::min(AUTO_BUDGET, (size_t)((nframes_all + n - 1u) / n) * frame_bytes);
         }
-        P.ring_mode = !bands && chunk < std::min<uint32_t>(std::max(count, 1u), 320u) ? 1u : 0u;
+        auto balanced = [&](size_t fit) {  // equal launches of at most `fit` frames
+            fit = std::max<size_t>(1, std::min<size_t>(fit, nframes_all));
+            const size_t n = (nframes_all + fit - 1u) / fit;
+            return (uint32_t)((nframes_all + n - 1u) / n);
+        };
+        uint32_t chunk = balanced(budget / frame_bytes), log2s = 0;
+        P.ring_mode = chunk < std::min(nframes_all, 320u) ? 1u : 0u;
         if (r->params.fold == RT_FOLD_BUFFER) P.ring_mode = 0u;  // forced (measurements, tests)
         if (r->params.fold == RT_FOLD_RING) P.ring_mode = 1u;
+        const size_t fail_above = (size_t)r->test_fail_alloc_above_mb << 20;
         size_t zero_words = 0;
         if (!P.ring_mode) {
             r->ring.release();  // the other fold's memory: the draw's colour memory stays within the budget
             r->ring_ctl.release();
-            // a device short of memory gets thinner bands, then fewer frames per launch, down to one frame, instead
-            // of a failed draw
-            for (;;) {
-                const size_t need = (size_t)bt * chunk * row_floats;
-                const size_t cap = std::max(bands ? budget / NBUF : budget, need * 4u);
-                rc = ensure_within(r->samples, need, cap, fail_above);
-                for (DevBuf<float>& b : r->band_buf)
-                    if (!rc && bands) rc = ensure_within(b, need, cap, fail_above);
-                if (rc != RT_ERR_ALLOC) break;
+            // a device short of memory gets smaller launches, down to one frame, instead of a failed draw
+            const size_t buf_budget = std::max(budget, frame_bytes);
+            while ((rc = ensure_within(r->samples, (size_t)chunk * frame_floats, buf_budget, fail_above)) == RT_ERR_ALLOC &&
+                   chunk > 1u) {
                 (void)hipGetLastError();  // clear the failed hipMalloc's sticky status
-                for (DevBuf<float>& b : r->band_buf) b.release();
-                if (bands && bt > 1u) {
-                    bt = (bt + 1u) / 2u;
-                } else if (chunk > 1u) {
-                    chunk = (chunk + 1u) / 2u;
-                } else {
-                    break;
-                }
+                chunk = (chunk + 1u) / 2u;
             }
             if (rc) return rc;
-            if (!bands)
-                for (DevBuf<float>& b : r->band_buf) b.release();
+            P.samples = r->samples.ptr;
             r->ring_slots = 0;
-            r->fold_bytes = (uint64_t)(bands ? NBUF : 1u) * bt * chunk * row_floats * 4u;
+            r->fold_bytes = (uint64_t)chunk * frame_bytes;
         } else {
             r->samples.release();
-            for (DevBuf<float>& b : r->band_buf) b.release();
             // frames per launch: at most FOLD_MAX_JOBS jobs per tile (the done bits of the tile's fold word)
             chunk = std::max(1u, std::min(count, hrt_dev::FOLD_MAX_JOBS * jf));
             const uint32_t nchunks_max = (chunk + jf - 1u) / jf;
@@ -662,115 +635,61 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                             4ull * zero_words + 8ull * ntiles;
         }
         // frame-block work stealing (rt_kernels.hip steal_block): the suspendable-walk kernels with the sample
-        // buffer; one slot per resident wave, at most 32 waves per CU (a half of the slots per side stream)
+        // buffer; one slot per resident wave, at most 32 waves per CU
         P.steal_cap = 32u * std::max(r->cus, 1u);
-        rc = ensure(r->steal_slots, 2u * (size_t)P.steal_cap);
+        rc = ensure(r->steal_slots, P.steal_cap);
         if (rc) return rc;
-        const uint32_t nrows_all = P.nrows, th_all = P.tiles_h;
-        float* const image0 = P.image;
-        const uint32_t nbands = bands ? (th_all + bt - 1u) / bt : 1u;
+        P.steal_slots = r->steal_slots.ptr;
+        P.queue = r->counter.ptr + 15u;
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
         r->last_suspend = split ? r->params.suspend_below : 0u;
         P.job_frames = jf;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
-        if (bands) {  // the side streams start after everything already on the renderer stream (zeroed counters)
-            HIP_TRY(hipEventRecord(r->ev_fork, r->stream));
-            for (hipStream_t sst : r->side) HIP_TRY(hipStreamWaitEvent(sst, r->ev_fork, 0));
-        }
-        // the drain fold needs every frame in one launch per band (each tile's frames folded by one launch); a band
-        // plan cut to frame chunks by a short device (the allocation loop above), and the opt-in SAH walk (k_trace<..,
-        // true> has no drain fold), run their bands on one stream, each folded by a k_accumulate right after it
-        const bool dfold = bands && chunk >= count && !P.tri_bvh;
-        float* const bufs[NBUF] = {r->samples.ptr, r->band_buf[0].ptr, r->band_buf[1].ptr, r->band_buf[2].ptr};
-        uint32_t li = 0;  // launch index
         for (uint32_t done = 0; done < count; done += chunk) {
-            for (uint32_t band = 0; band < nbands; band++, li++) {
-                const uint32_t k = dfold ? (li & 1u) : 0u;   // side stream of this launch
-                const uint32_t kb = bands ? li % NBUF : 0u;  // and its buffer
-                P.kr0 = band * bt * 8u;
-                P.nrows = bands ? std::min(bt * 8u, nrows_all - P.kr0) : nrows_all;
-                P.tiles_h = bands ? (P.nrows + 7u) / 8u : th_all;
-                P.image = image0 + (size_t)P.kr0 * r->width * 3u;
-                P.samples = P.ring_mode ? nullptr : bufs[kb];
-                P.queue = r->counter.ptr + (k ? hrt_dev::QUEUE2 : 15u);
-                P.steal_slots = r->steal_slots.ptr + (size_t)k * P.steal_cap;
-                // band li - 2 (this stream's previous launch: complete when this one starts) is folded in this drain
-                P.dfold_samples = nullptr;
-                P.dfold_image = nullptr;
-                P.dfold_next = nullptr;
-                P.dfold_tiles = P.dfold_nrows = 0u;
-                if (dfold && band >= 2u) {
-                    const uint32_t pkr0 = (band - 2u) * bt * 8u;
-                    P.dfold_samples = bufs[(li - 2u) % NBUF];
-                    P.dfold_image = image0 + (size_t)pkr0 * r->width * 3u;
-                    P.dfold_nrows = std::min(bt * 8u, nrows_all - pkr0);
-                    P.dfold_tiles = P.tiles_w * ((P.dfold_nrows + 7u) / 8u);
-                    P.dfold_next = r->counter.ptr + hrt_dev::DFOLD + k;
-                }
-                P.nframes = std::min(chunk, count - done);
-                P.time0 = time0 + done * dtime;
-                P.frame0 = r->frame_count + done;
-                P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
-                const uint32_t lt = P.tiles_w * P.tiles_h;  // tiles of this launch
-                P.njobs = (unsigned long long)lt * P.nchunks;
-                // Auto stealing: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job
-                // dealt late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for
-                // long launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 ->
-                // 0.88), and for pipelined bands but the last, whose drains the next band fills
-                {
-                    const bool fits = lt < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
-                    const bool covered = dfold && band + 1u < nbands;
-                    const bool want = r->params.steal == 2u ||
-                                      (r->params.steal == 0u && !covered && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
-                    P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
-                }
-                // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
-                // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
-                // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
-                P.tail_from = 0xFFFFFFFFu;
-                const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
-                if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
-                    r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
-                    const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
-                    P.tail_from = (uint32_t)(P.njobs - q);
-                    P.njobs += 3ull * q;
-                }
-                r->ring_nchunks = P.nchunks;
-                hipStream_t st = bands ? r->side[k] : r->stream;
-                HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), st));
-                if (P.dfold_next) HIP_TRY(hipMemsetAsync(P.dfold_next, 0, sizeof(unsigned long long), st));
-                if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), st));
-                if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), st));
-                rc = trace_events(r, r->trace_pairs_pending);
-                if (rc) return rc;
-                HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], st));
-                HIP_TRY(hrt_launch_trace(r->mode, variant, P, st));
-                HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], st));
-                r->trace_pairs_pending++;
+            P.nframes = std::min(chunk, count - done);
+            P.time0 = time0 + done * dtime;
+            P.frame0 = r->frame_count + done;
+            P.nchunks = (P.nframes + P.job_frames - 1u) / P.job_frames;
+            P.njobs = (unsigned long long)ntiles * P.nchunks;
+            // Auto stealing: on for launches with fewer than 16 jobs per resident wave (about 24 per CU), where a job
+            // dealt late can outlast the launch (C4's 8-way split: 0.47 -> 0.71 of the full image's rate); off for
+            // long launches, where the claims cost 2-4 % and there is no tail to win back (C3: 8-way split 0.90 ->
+            // 0.88)
+            {
+                const bool fits = ntiles < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
+                const bool want = r->params.steal == 2u ||
+                                  (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
+                P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
+            }
+            // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
+            // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
+            // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
+            P.tail_from = 0xFFFFFFFFu;
+            const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
+            if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
+                r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
+                const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
+                P.tail_from = (uint32_t)(P.njobs - q);
+                P.njobs += 3ull * q;
+            }
+            r->ring_nchunks = P.nchunks;
+            HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
+            if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
+            if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
+            rc = trace_events(r, r->trace_pairs_pending);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
+            HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
+            HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
+            r->trace_pairs_pending++;
+            launches++;
+            if (!P.ring_mode) {
+                HIP_TRY(hrt_launch_accumulate(P, r->stream));
                 launches++;
-                // the sample buffer of a launch no later band folds in its drain: k_accumulate after it, same stream
-                if (!P.ring_mode && (!dfold || band + 2u >= nbands)) {
-                    HIP_TRY(hrt_launch_accumulate(P, st));
-                    launches++;
-                }
             }
         }
-        if (bands) {  // the renderer stream (ev_stop, readback) waits for both side streams
-            for (uint32_t k = 0; k < 2u; k++) {
-                HIP_TRY(hipEventRecord(r->ev_tdone[k], r->side[k]));
-                HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_tdone[k], 0));
-            }
-        }
-        P.dfold_samples = nullptr;
-        P.dfold_image = nullptr;
-        P.dfold_next = nullptr;
-        P.dfold_tiles = P.dfold_nrows = 0u;
-        P.kr0 = 0u;
-        P.nrows = nrows_all;
-        P.tiles_h = th_all;
-        P.image = image0;
-        r->stats_bands = nbands;
+        r->last_launch_frames = chunk;
         r->trace_pairs = r->trace_pairs_pending;
         r->trace_pairs_pending = 0;
     } else {
@@ -795,7 +714,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     if (schedule == RT_SCHEDULE_QUEUE && count && P.nrows) {
         r->stats.fold_ring = P.ring_mode;
         r->stats.fold_bytes = r->fold_bytes;
-        r->stats.bands = r->stats_bands;
+        r->stats.launch_frames = std::min(count, r->last_launch_frames);
     }
     r->stats.device_bytes = r->device_bytes();
     r->timing_pending = true;
@@ -879,7 +798,6 @@ void delete_buffers(rt_renderer* r) {
     r->counter.release();
     r->steal_slots.release();
     r->samples.release();
-    for (DevBuf<float>& b : r->band_buf) b.release();
     r->ring.release();
     r->ring_ctl.release();
     r->wave_trace.release();
@@ -931,8 +849,8 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.row_block = 1;
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
-    // 32 GiB of the 288 GB HBM: all 1024 C3 frames in one launch (pipelined bands: launch_frames)
-    r->params.queue_budget_mb = 32768;
+    // auto: balanced launches of 320-639 frames (C3: 3 x 342 frames, 8.5 GB of colours; launch_frames)
+    r->params.queue_budget_mb = 0;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16
     r->params.job_frames = 0;  // per kernel (rt_draw_frames)
@@ -941,11 +859,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92
     r->params.suspend_below = mode == RT_MODE_SPHERE ? 24u : 32u;
     bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreate(&r->ev_start) == hipSuccess && hipEventCreate(&r->ev_stop) == hipSuccess &&
-              hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; k < 2 && ok; k++)
-        ok = hipStreamCreateWithFlags(&r->side[k], hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&r->ev_tdone[k], hipEventDisableTiming) == hipSuccess;
+              hipEventCreate(&r->ev_start) == hipSuccess && hipEventCreate(&r->ev_stop) == hipSuccess;
     if (!ok) {
         rt_destroy(r);
         return fail(RT_ERR_DEVICE, "rt_create: stream/event creation failed");
@@ -963,17 +877,10 @@ int rt_destroy(rt_renderer* r) {
     if (!r) return RT_OK;
     DeviceScope ds(r->device);  // (frees on the renderer's device even if switching failed)
     if (r->stream) (void)hipStreamSynchronize(r->stream);
-    for (hipStream_t s : r->side)
-        if (s) (void)hipStreamSynchronize(s);
     delete_buffers(r);
     for (hipEvent_t e : r->ev_trace) (void)hipEventDestroy(e);
     if (r->ev_start) (void)hipEventDestroy(r->ev_start);
     if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
-    if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
-    for (int k = 0; k < 2; k++) {
-        if (r->ev_tdone[k]) (void)hipEventDestroy(r->ev_tdone[k]);
-        if (r->side[k]) (void)hipStreamDestroy(r->side[k]);
-    }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;
@@ -1210,7 +1117,6 @@ int rt_release_scratch(rt_renderer* r) {
     }
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->samples.release();
-    for (DevBuf<float>& b : r->band_buf) b.release();
     r->ring.release();
     r->ring_ctl.release();
     return RT_OK;

@@ -77,11 +77,9 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 
 // Small culling BVHs (<= LNODE_CAP nodes, depth <= LNODE_DEPTH) are read from LDS by k_trace_split<true>
 // (renderer.cpp decides, the kernel bounds its copy by the same constant).
-// device counter words: [0, 16) exported (include/hrt.h RT_RAW_COUNTERS; [15] = the job queue of the first
-// stream), then the fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue
-// overruns; [20] the job queue of the second stream (pipelined band launches, renderer.cpp), [21, 23) the drain
-// fold's tile claims of the two streams
-constexpr uint32_t WATCHDOG = 16, QUEUE2 = 20, DFOLD = 21, COUNTER_WORDS = 23;
+// device counter words: [0, 16) exported (include/hrt.h RT_RAW_COUNTERS; [15] = the job queue), then the
+// fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue overruns
+constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
 
 // fold ring: jobs per tile and launch (the done bits of a tile's fold word, rt_kernels.hip)
 constexpr uint32_t FOLD_MAX_JOBS = 48;
@@ -160,11 +158,7 @@ struct KParams {
     uint32_t jf_log2, pad_r;      // job_frames = 1 << jf_log2
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames), + 3 per job split in quarters
-    uint32_t tail_from;           // sample buffer: jobs from this index on are quarter jobs (4 per original job)
-    // The launch covers local rows kr0 .. kr0 + nrows - 1 of the renderer (a band of the sample buffer's pipelined
-    // launches, renderer.cpp; 0 otherwise): kernels index the image (based at that band) and the tiles by the
-    // band-local row kr, and seed / aim the camera with the renderer-local row kr0 + kr
-    uint32_t kr0;
+    uint32_t tail_from, pad_t;    // sample buffer: jobs from this index on are quarter jobs (4 per original job)
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
     uint32_t job_frames, nchunks; // frames per job (a job = one tile x job_frames frames), chunks per tile
     uint32_t suspend_below;       // k_trace_split: suspend the walks once fewer lanes than this still walk
@@ -173,13 +167,6 @@ struct KParams {
     unsigned long long* steal_slots;  // one per wave: (job + 1) << 32 | frames claimed; zeroed per launch
     uint32_t steal, nwaves;       // on; waves of the launch (launch_persistent)
     uint32_t steal_cap, pad_s;    // slots allocated (bounds the grid)
-    // drain fold (pipelined bands, renderer.cpp): once its jobs are done, each wave of a band launch folds tiles of
-    // the band launched two before it on the same stream (complete by stream order) into the image before it
-    // exits — the fold runs in this launch's drain, not in a k_accumulate that competes with the next band's waves
-    const float* dfold_samples;   // that band's sample buffer; nullptr: no drain fold
-    float* dfold_image;           // its first image row
-    unsigned long long* dfold_next;  // tile claims (zeroed per launch)
-    uint32_t dfold_tiles, dfold_nrows;  // its tiles (tiles_w x its tile rows) and rows; frames as this launch's
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

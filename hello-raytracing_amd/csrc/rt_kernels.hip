@@ -1146,7 +1146,7 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
 }
 
 // Folds the sample buffer's colours of one tile's pixels into the image in frame order with the mix k_render uses
-// (WGSL mix, shader_sphere.wgsl:264-271) — k_accumulate and the bands' drain fold. `tile` (wave-uniform) points at the
+// (WGSL mix, shader_sphere.wgsl:264-271) for k_accumulate. `tile` (wave-uniform) points at the
 // tile's frame 0, frame f at tile + f * fstride; the lane's pixel is 3 floats at lane3. U frames' loads are issued
 // before their mixes (a wave's frame is 768 B: one load in flight per wave left k_accumulate latency-bound); the
 // uniform frame address + a 32-bit lane offset keeps each load to one VGPR of address (global_load saddr).
@@ -1183,27 +1183,6 @@ __device__ __forceinline__ void fold_pixel(float* px, const float* tile, uint32_
     px[0] = acc0;
     px[1] = acc1;
     px[2] = acc2;
-}
-
-// The drain fold of a band launch (KParams dfold_*): after its own jobs, the wave claims whole tiles of the earlier
-// band (one pixel per lane, every frame in order) until none is left. Reached by every wave of the launch (after its
-// job loop), so each claimed tile is folded exactly once before the launch ends.
-template <int U = 4>
-__device__ __forceinline__ void drain_fold(uint32_t lane) {
-    const KPtr K = kargs();
-    if (K->dfold_samples == nullptr) return;
-    const uint32_t ntiles = K->dfold_tiles, tw = K->tiles_w;
-    const size_t fstride = (size_t)ntiles * 64u * 3u;
-    while (true) {
-        uint32_t t = 0;
-        if (lane == 0) t = (uint32_t)min(atomicAdd(K->dfold_next, 1ull), 0xFFFFFFFFull);
-        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0));  // (every lane holds lane 0's claim)
-        if (t >= ntiles) break;
-        const uint32_t x = (t % tw) * 8u + (lane & 7u), kr = (t / tw) * 8u + (lane >> 3);
-        if (x < K->W && kr < K->dfold_nrows)
-            fold_pixel<U>(K->dfold_image + ((size_t)kr * K->W + x) * 3u, K->dfold_samples + (size_t)t * 192u, lane * 3u,
-                          fstride, K->nframes, K->frame0, K->ema_cap);
-    }
 }
 
 #ifdef HRT_RINGSTAT
@@ -1559,7 +1538,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             const uint32_t kr = (B.job_tile / P.tiles_w) * 8u + (lane >> 3);
             B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             if (B.pr_ok) {
-                const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, P.kr0 + kr);
+                const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
                 const Ray pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
                 B.pr_o = pr.o;
                 B.pr_d = pr.d;
@@ -1610,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t kr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool valid = x < P.W && kr < P.nrows;
-    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, P.kr0 + kr);
+    const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
     float* px = P.image + ((size_t)kr * P.W + x) * 3u;
 
     float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
@@ -1824,7 +1803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t kr = (job_tile / HRT_KF(tiles_w)) * 8u + (l >> 3);
                 need = false;
                 if (x < HRT_KF(W) && kr < HRT_KF(nrows)) {  // ragged edge tiles: samples outside the image are skipped
-                    const uint32_t y = global_row(HRT_KF(row0), HRT_KF(row_block), HRT_KF(row_stride), HRT_KF(kr0) + kr);
+                    const uint32_t y = global_row(HRT_KF(row0), HRT_KF(row_block), HRT_KF(row_stride), kr);
                     ray = primary_ray<MODE>(&kargs()->cam, x, y, HRT_KF(time0) + (job_f0 + (sid >> 6)) * HRT_KF(dtime), s);
 #undef HRT_KF
                     sky_t = ray.d.y * 0.5f + 0.5f;
@@ -1888,9 +1867,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #endif
         job_account(J, fin, fl, lane);
     }
-    // (not in the SAH-walk instantiations, where the fold's code cost a wave per SIMD: renderer.cpp folds their
-    // bands with k_accumulate)
-    if constexpr (!TSAH) drain_fold<2>(lane);
 #ifdef HRT_STAMPS
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
@@ -1971,7 +1947,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
             uint32_t ps = 0;
             if (pok) {
-                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, K->kr0 + kr);
+                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
                 pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
             }
             blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
@@ -2122,7 +2098,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 uint32_t ps = 0;
                 if (pok) {
                     const KPtr K = kargs();  // row map and time: loaded here, not held in SGPRs
-                    const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, K->kr0 + kr);
+                    const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
                     pr = primary_ray<MODE>(&K->cam, x, y, K->time0 + (job_f0 + blk_f) * K->dtime, ps);
                 }
                 blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
@@ -2222,7 +2198,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_PHASE(3);
     }
     HRT_PHASE_FLUSH
-    drain_fold(lane);
 #if defined(HRT_STAMPS) && !defined(HRT_PHASES)
     {
         unsigned long long v[7] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
@@ -2381,7 +2356,6 @@ k_trace_split_tris(const KParams P) {
         HRT_PHASE(3);
     }
     HRT_PHASE_FLUSH
-    drain_fold(lane);
 #ifdef HRT_RINGSTAT
     if (lane == 0)
         for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));

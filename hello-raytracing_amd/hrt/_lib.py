@@ -70,7 +70,7 @@ class RtStats(C.Structure):
         ("kernel", C.c_char * 64),
         ("fold_bytes", C.c_uint64),
         ("fold_ring", C.c_uint32),
-        ("bands", C.c_uint32),
+        ("launch_frames", C.c_uint32),
         ("device_bytes", C.c_uint64),
     ]
 

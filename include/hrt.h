@@ -71,12 +71,12 @@ typedef struct rt_params {
                                   launch's frames, in-register accumulation), 2 sample queue (persistent
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
-    uint32_t queue_budget_mb;  /* sample-queue colour memory in MiB; default 32768. The sample buffer: one
-                                  launch when a draw's colours fit; else bands of tile rows x every frame in
-                                  four buffers of a quarter of the budget, pipelined over two streams (each
-                                  band folds the band two before it in its drain); else launches of as many
-                                  frames as fit, or the fold ring below min(frames, 320) frames (bounded
-                                  memory, slower)                                          */
+    uint32_t queue_budget_mb;  /* sample-queue colour memory: 0 (default) auto = the sample buffer in
+                                  floor(frames / 320) balanced launches (at least one): 320-639 frames of
+                                  colours, at most 32 GiB (C3: 3 x 342 frames, 8.5 GB); else a cap in MiB:
+                                  balanced launches of as many frames as it holds. The fold ring (bounded
+                                  memory, slower) when a launch would get fewer than min(frames, 320)
+                                  frames                                                   */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
                                   power of two (at most 1024); default 0 = per kernel: 32 with the
                                   suspendable walks, 16 for the linear sphere scans                      */
@@ -141,8 +141,8 @@ typedef struct rt_stats {
                               job_frames x 64 px x 16 B plus control words); 0 for the tiles schedule    */
     uint32_t fold_ring;    /* 1: the last draw folded through the fold ring (bounded memory), 0: through the
                               sample buffer and k_accumulate (rt_params.queue_budget_mb decides)         */
-    uint32_t bands;        /* sample buffer: row bands the last draw's launches covered (1 = every launch covers all
-                              of the renderer's rows; > 1 = pipelined band launches, rt_params.queue_budget_mb) */
+    uint32_t launch_frames; /* sample queue: frames per trace launch of the last draw (the last launch may
+                              have fewer; rt_params.queue_budget_mb)                                   */
     uint64_t device_bytes; /* device memory the renderer holds after the last draw call (image, scene,
                               colour fold, counters): the fold's share stays within queue_budget_mb      */
 } rt_stats;

@@ -179,18 +179,20 @@ def test_sample_queue_chunks_and_tris_mode():
         assert (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), st.fold_bytes
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 320 MiB hold 364 frames (>= 320: the sample buffer)
-    # -> 700 frames in launches of 364 and 336
+    # -> 700 frames in two balanced launches of 350; the default budget (auto: floor(700 / 320) = 2 launches) the
+    # same; 1000 MiB hold all 700 frames: one launch
     per_frame = 1200 * 64 * 12
-    chunk = (320 << 20) // per_frame
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
     ref.draw_frames(700, 1000, 10)
-    r = scenes.make_renderer(sd)
-    r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=320)
-    r.draw_frames(700, 1000, 10)
-    st = r.stats()
-    assert st.fold_ring == 0 and st.launches == 4 and st.fold_bytes == chunk * per_frame, (st.launches, st.fold_bytes)
-    np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
+    for mb, nl, chunk in ((320, 2, 350), (None, 2, 350), (1000, 1, 700)):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **({"queue_budget_mb": mb} if mb else {}))
+        r.draw_frames(700, 1000, 10)
+        st = r.stats()
+        assert st.fold_ring == 0 and st.launches == 2 * nl and st.trace_launches == nl, (mb, st.launches)
+        assert st.launch_frames == chunk and st.fold_bytes == chunk * per_frame, (mb, st.launch_frames, st.fold_bytes)
+        np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     scene = hrt.SceneTris.new_suzane(96, 72)
     scene.init()
     sd = scenes.SceneDef("suzane", hrt.RT_MODE_TRIS, 96, 72, scene.camera, bvh=scene.tris_bvh.view(), frames=4)
@@ -231,53 +233,6 @@ def test_fold_allocation_failure_shrinks_the_launches():
     assert st.launches == 2 and st.fold_bytes > 100 << 20
     np.testing.assert_array_equal(small.view(np.uint32), want.view(np.uint32))
     np.testing.assert_array_equal(ring.view(np.uint32), want.view(np.uint32))
-
-
-@pytest.mark.parametrize("case", ["c3", "c4", "rows", "steal", "chunked"])
-def test_band_pipeline_bit_identical(case):
-    """Sample-buffer draws whose colours exceed the budget run as pipelined BANDS (renderer.cpp launch_frames): launches
-    of tile-row bands x every frame on two side streams with four buffers of a quarter of the budget; band i's waves
-    fold band i - 2 in their drain (rt_kernels.hip drain_fold), the last two bands get a k_accumulate. Images and every
-    work count equal the single-launch draw (32 GiB budget) and the oracle on sampled rows; the colour memory stays
-    within the budget; ragged last bands, a row partition (8-row blocks of rank 1 of 3), stealing on short band
-    launches, the triangle / mixed heap walk, and a device too short for one tile row x every frame (fault injection:
-    frame chunks of bands on one stream, a k_accumulate after each) included."""
-    fault = {}
-    if case == "c3":
-        sd, extra, budget = scenes.config_c3(1920, 1080, 64), {"job_frames": 16}, 1100  # 6 bands: 5 x 23 + 20 tile rows
-    elif case == "c4":
-        sd, extra, budget = scenes.config_c4(1280, 720, 24), {"job_frames": 2}, 150   # 7 bands: 6 x 13 + 12
-    elif case in ("rows", "chunked"):
-        from hrt.parallel import rank_params
-        sd, extra, budget = scenes.config_c3(1280, 720, 32), {**rank_params(1, 3, 8), "job_frames": 1}, 64  # 8: 7 x 4 + 2
-        if case == "chunked":  # one tile row x 32 frames is 3.9 MB: bands of one tile row x 16 frames
-            fault = {"fail_alloc_above_mb": 2}
-    else:
-        sd, extra, budget = scenes.config_c3(960, 544, 16), {"job_frames": 1, "steal": 2}, 56  # 8: 7 x 9 + 5
-    runs = []
-    for mb in (32768, budget):
-        r = scenes.make_renderer(sd)
-        if mb == budget and fault:
-            r.set_faults(**fault)
-        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, queue_budget_mb=mb, **extra)
-        r.draw_frames(sd.frames, 1000, 10)
-        st = r.stats()
-        runs.append((r.read_image(), st))
-    (one, st1), (band, stb) = runs
-    assert st1.bands == 1 and stb.bands > 1 and stb.fold_ring == 0, (case, st1.bands, stb.bands, stb.fold_ring)
-    if case == "chunked":
-        assert stb.bands == 30 and stb.trace_launches == 2 * stb.bands and stb.launches == 2 * stb.trace_launches, stb
-    else:
-        assert stb.trace_launches == stb.bands and stb.launches == stb.bands + 2, (case, stb.launches, stb.bands)
-    assert stb.fold_bytes <= budget << 20, (case, stb.fold_bytes)
-    assert stb.device_bytes - stb.fold_bytes < st1.device_bytes  # the whole-draw buffer is gone
-    np.testing.assert_array_equal(one.view(np.uint32), band.view(np.uint32), err_msg=case)
-    assert (st1.queries, st1.node_tests, st1.tri_tests, st1.sphere_tests) == \
-        (stb.queries, stb.node_tests, stb.tri_tests, stb.sphere_tests), case
-    if case in ("c3", "c4"):  # every 97th row against the oracle
-        step = 97
-        ref, _ = scenes.oracle_render(sd, rows=(3, step, len(range(3, sd.height, step))))
-        assert_parity(band[3::step], ref, f"band pipeline {case}")
 
 
 def test_fold_memory_follows_the_budget():
