@@ -161,6 +161,8 @@ struct rt_renderer {
     DevBuf<int> bvh_slot, bvh_large;
     hrt::SphereBvh bvh_host;
     DevBuf<float4> nodes;
+    DevBuf<float> nodes_so;  // the same nodes as (lo, hi, lo) per axis (pack_nodes_so)
+    bool so_ok = false;
     DevBuf<hrt_dev::TriDev> tris;
     DevBuf<hrt_dev::MatDev> mats;
     uint32_t bvh_n = 0, bvh_m = 0;
@@ -201,7 +203,7 @@ struct rt_renderer {
     uint32_t row_block() const { return std::max(params.row_block, 1u); }
     uint64_t device_bytes() const {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
-               bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + tris.bytes() + mats.bytes() +
+               bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes();
     }
@@ -250,6 +252,26 @@ std::vector<float4> pack_bvh_nodes(const std::vector<hrt::SphereBvhNode>& nodes,
         o[1] = float4{rel_hi(n.lmax[0], 0), rel_hi(n.lmax[1], 1), rel_hi(n.lmax[2], 2), 0.0f};
         o[2] = float4{rel_lo(n.rmin[0], 0), rel_lo(n.rmin[1], 1), rel_lo(n.rmin[2], 2), __builtin_bit_cast(float, n.right)};
         o[3] = float4{rel_hi(n.rmax[0], 0), rel_hi(n.rmax[1], 1), rel_hi(n.rmax[2], 2), 0.0f};
+    }
+    return out;
+}
+
+// The heap's nodes for the sign-ordered node test (rt_kernels.hip node_hit_so; tests/test_sign_ordered_slab.py):
+// (lo, hi, lo) per axis, 9 floats per node, with lo <= hi — an axis with min > max (padding nodes: +MAX / -MAX) is
+// swapped, which changes nothing in intersect_node (shader_tris.wgsl:150-159: min / max take the pair in either order).
+// A NaN bound leaves its axis as given and clears so_ok (the kernels then use the reference form on this layout).
+std::vector<float> pack_nodes_so(const float* nodes, uint32_t n, bool& so_ok) {
+    std::vector<float> out(9 * (size_t)std::max<uint32_t>(n, 1), 0.0f);
+    so_ok = true;
+    for (uint32_t i = 0; i < n; i++) {
+        for (int k = 0; k < 3; k++) {
+            float lo = nodes[8 * (size_t)i + k], hi = nodes[8 * (size_t)i + 4 + k];
+            if (std::isnan(lo) || std::isnan(hi)) so_ok = false;
+            else if (lo > hi) std::swap(lo, hi);
+            out[9 * (size_t)i + 3 * k] = lo;
+            out[9 * (size_t)i + 3 * k + 1] = hi;
+            out[9 * (size_t)i + 3 * k + 2] = lo;
+        }
     }
     return out;
 }
@@ -470,6 +492,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.sph_geo = r->sph_geo.ptr;
     P.sph_aux = r->sph_aux.ptr;
     P.nodes = r->nodes.ptr;
+    P.nodes_so = r->nodes_so.ptr;
+    P.so_ok = r->so_ok ? 1u : 0u;
     P.tris = r->tris.ptr;
     P.tri_bvh = (r->mode != RT_MODE_SPHERE && r->params.tri_bvh) ? 1u : 0u;
     if (P.tri_bvh) {
@@ -791,6 +815,7 @@ void delete_buffers(rt_renderer* r) {
     r->bvh_slot.release();
     r->bvh_large.release();
     r->nodes.release();
+    r->nodes_so.release();
     r->tris.release();
     r->mats.release();
     r->tb_hnodes.release();
@@ -979,17 +1004,22 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
         md[k] = hrt_dev::MatDev{M[k].albedo.x, M[k].albedo.y, M[k].albedo.z, M[k].params.x, M[k].kind,
                                 dc.inv_param, dc.r0sq_front, dc.r0sq_back};
     }
+    bool so_ok = true;
+    const std::vector<float> so = pack_nodes_so((const float*)nodes32, n, so_ok);
     int rc = ensure(r->nodes, 2 * (size_t)std::max<uint32_t>(n, 1));
+    if (!rc) rc = ensure(r->nodes_so, so.size());
     if (!rc) rc = ensure(r->tris, std::max<uint32_t>(m, 1));
     if (!rc) rc = ensure(r->mats, std::max<uint32_t>(n_mats, 1));
     if (rc) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(r->nodes.ptr, nodes32, (size_t)n * 32u, hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipMemcpyAsync(r->nodes_so.ptr, so.data(), so.size() * sizeof(float), hipMemcpyHostToDevice, r->stream));
     if (m) HIP_TRY(hipMemcpyAsync(r->tris.ptr, td.data(), (size_t)m * sizeof(td[0]), hipMemcpyHostToDevice, r->stream));
     if (n_mats)
         HIP_TRY(hipMemcpyAsync(r->mats.ptr, md.data(), (size_t)n_mats * sizeof(md[0]), hipMemcpyHostToDevice, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->bvh_n = n;
     r->bvh_m = m;
+    r->so_ok = so_ok;
     return RT_OK;
 }
 

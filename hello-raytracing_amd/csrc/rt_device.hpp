@@ -167,6 +167,10 @@ struct KParams {
     unsigned long long* steal_slots;  // one per wave: (job + 1) << 32 | frames claimed; zeroed per launch
     uint32_t steal, nwaves;       // on; waves of the launch (launch_persistent)
     uint32_t steal_cap, pad_s;    // slots allocated (bounds the grid)
+    // the heap's nodes as (lo, hi, lo) per axis, 9 floats per node (renderer.cpp pack_nodes_so; the heap-top kernels'
+    // sign-ordered node test, rt_kernels.hip node_hit_so); so_ok 0: a NaN bound, the reference form only
+    const float* nodes_so;
+    uint32_t so_ok, pad_so;
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

@@ -532,19 +532,67 @@ __device__ __forceinline__ bool node_hit(const KParams& P, uint32_t i, const f3&
 // from L1/L2 in the same step, merged by selects (C4 -4.6 %, C5 -2 %): the extra selects, and the wave still waits
 // for the slowest load of the step. The nodes below the top are read through a buffer descriptor: plain global
 // loads in the other arm get merged with the LDS loads into flat loads of a selected pointer.
-template <uint32_t HT>
-__device__ __forceinline__ bool node_hit_top(const KParams& P, const float4* __restrict__ top, uint32_t i, const f3& o,
-                                             const f3& inv) {
-    if constexpr (HT > 0) {
-        if (__ballot(i >= HT) == 0ull) return node_slab(top[2 * i], top[2 * i + 1], o, inv);
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.n * 32u), 0x00020000);
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 32u), 0, 0);
-        const f4v b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 32u + 16u), 0, 0);
-        return node_slab(float4{a.x, a.y, a.z, a.w}, float4{b.x, b.y, b.z, b.w}, o, inv);
+
+// Sign-ordered node test (the heap-top kernels, HT > 0; tests/test_sign_ordered_slab.py). The nodes are laid out as
+// (lo, hi, lo) per axis, 36 B per node, lo <= hi (renderer.cpp pack_nodes_so swaps padding / inverted axes: the
+// reference's min / max take the pair in either order). Reading two floats at axis * 12 + 4 * (1/d < 0) gives the
+// near plane, then the far one, so each axis needs no min / max:
+//   max3(tnear) <= min3(tfar) && min3(tfar) >= 0  ==  intersect_node (shader_tris.wgsl:150-159)
+// whenever 1/d and the origin are finite and no bound is NaN (with lo <= hi and a finite nonzero 1/d, RN keeps
+// (lo - o) / d and (hi - o) / d in the order of the sign of 1/d, so min / max would pick exactly those two; zeros of
+// either sign only reach comparisons). A wave with any non-finite 1/d or origin (a direction component of +-0 or
+// below 2^-126: 0 x inf), or a tree with a NaN bound (KParams so_ok 0), uses the reference form on the same layout
+// (lo, hi at axis * 12). 6 VALU fewer per node test for 3 address multiply-adds (the per-lane offsets ox, oy, oz).
+constexpr uint32_t SO_NODE_BYTES = 36;
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ bool node_slab_so(const f2v x, const f2v y, const f2v z, const f3& o, const f3& inv) {
+    const float tnx = (x.x - o.x) * inv.x, tny = (y.x - o.y) * inv.y, tnz = (z.x - o.z) * inv.z;
+    const float tfx = (x.y - o.x) * inv.x, tfy = (y.y - o.y) * inv.y, tfz = (z.y - o.z) * inv.z;
+    const float tmin = fmax_ieee(fmax_ieee(tnx, tny), tnz);
+    const float tmax = fmin_ieee(fmin_ieee(tfx, tfy), tfz);
+    return tmin <= tmax && tmax >= 0.0f;
+}
+__device__ __forceinline__ bool node_slab_lohi(const f2v x, const f2v y, const f2v z, const f3& o, const f3& inv) {
+    return node_slab(float4{x.x, y.x, z.x, 0.0f}, float4{x.y, y.y, z.y, 0.0f}, o, inv);
+}
+__device__ __forceinline__ f2v lds_pair(uint32_t a) {
+    return f2v{*(const lds_f32*)(uintptr_t)a, *(const lds_f32*)(uintptr_t)(a + 4u)};
+}
+__device__ __forceinline__ f2v buf_pair(__amdgpu_buffer_rsrc_t rs, uint32_t a) {
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)a, 0, 0);
+    return f2v{__uint_as_float(v.x), __uint_as_float(v.y)};
+}
+
+// nodes_so based at -tb (the LDS top's byte addresses reach the same node), from fresh scalar loads (four SGPRs held
+// across the walk spilled in the C5 kernel)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t so_rsrc(uint32_t tb) {
+    const KPtr K = kargs();
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)K->nodes_so - tb), (short)0,
+                                             (int)(K->n * SO_NODE_BYTES + tb), 0x00020000);
+}
+
+// Node i through the sign-ordered layout: from the LDS top (nodes 0 .. HT - 1, byte address tb + i * 36) when every
+// walking lane of the wave is inside it, else through nodes_so (so_rsrc: the same byte addresses). The pairs at
+// ox / oy / oz (+ i * 36): SO, tb + axis * 12 + 4 * (1/d < 0), near then far; else tb + axis * 12, lo then hi, tested
+// with the reference's min / max. (One loop with a wave-uniform branch between the two tests, instead of two
+// instantiations of the walk, measured C4 -1.5 %, C5 -1.2 %.)
+template <uint32_t HT, bool SO, bool FULL = false>
+__device__ __forceinline__ bool node_hit_so(uint32_t i, const f3& o, const f3& inv, uint32_t tb, uint32_t ox, uint32_t oy,
+                                            uint32_t oz) {
+    const bool lds = FULL || __ballot(i >= HT) == 0ull;  // FULL: every internal node is in the top (n <= HT)
+    const uint32_t ax = __umul24(i, SO_NODE_BYTES) + ox, ay = __umul24(i, SO_NODE_BYTES) + oy,
+                   az = __umul24(i, SO_NODE_BYTES) + oz;
+    if constexpr (SO) {
+        if (lds) return node_slab_so(lds_pair(ax), lds_pair(ay), lds_pair(az), o, inv);
+        const __amdgpu_buffer_rsrc_t rs = so_rsrc(tb);
+        return node_slab_so(buf_pair(rs, ax), buf_pair(rs, ay), buf_pair(rs, az), o, inv);
     } else {
-        return node_hit(P, i, o, inv);
+        if (lds) return node_slab_lohi(lds_pair(ax), lds_pair(ay), lds_pair(az), o, inv);
+        const __amdgpu_buffer_rsrc_t rs = so_rsrc(tb);
+        return node_slab_lohi(buf_pair(rs, ax), buf_pair(rs, ay), buf_pair(rs, az), o, inv);
     }
 }
 
@@ -644,12 +692,22 @@ constexpr uint32_t PAIR_BIT = 0x80000000u;
 // triangles.)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;  // 32-bit LDS addressing for the list
 
-template <bool SUSPEND, uint32_t HT = 0, uint32_t LS = 256, uint32_t CAP = TRI_BATCH, bool TBUF = false>
+template <bool SUSPEND, uint32_t HT = 0, uint32_t LS = 256, uint32_t CAP = TRI_BATCH, bool TBUF = false, bool SO = false,
+          bool FULL = false>
 __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWalk& W, Tally& tally, uint32_t* cand_g,
-                                         uint32_t below, const float4* __restrict__ top = nullptr) {
+                                         uint32_t below, const float* __restrict__ top = nullptr) {
     // the list's LDS byte address (32-bit arithmetic): entry k at c0 + k * 4 LS
     const uint32_t c0 = (uint32_t)(uintptr_t)(lds_u32*)cand_g;
     const f3 inv = W.inv;
+    // HT > 0: the sign-ordered layout (node_hit_so), LDS top at byte address tb
+    uint32_t tb = 0u, ox = 0u, oy = 0u, oz = 0u;
+    if constexpr (HT > 0) {
+        tb = (uint32_t)(uintptr_t)(const lds_f32*)top;
+        const uint32_t sm = SO ? 4u : 0u;  // (the sign offsets only with the sign-ordered test)
+        ox = tb + ((__float_as_uint(inv.x) >> 29) & sm);
+        oy = tb + 12u + ((__float_as_uint(inv.y) >> 29) & sm);
+        oz = tb + 24u + ((__float_as_uint(inv.z) >> 29) & sm);
+    }
     const uint32_t n = P.n, m = P.m;
     uint32_t i = W.i, step = W.step, nc = 0u;
     const uint32_t step0 = step, tris0 = tally.tris;
@@ -668,7 +726,9 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
     while (true) {
         while (walking != 0u && __ballot(nc == CAP) == 0ull) {
             step++;
-            const bool hit = node_hit_top<HT>(P, top, i, r.o, inv);
+            bool hit;
+            if constexpr (HT > 0) hit = node_hit_so<HT, SO, FULL>(i, r.o, inv, tb, ox, oy, oz);
+            else hit = node_hit(P, i, r.o, inv);
             const bool down = hit && 2u * i < n;
             if (hit && !down) {  // bottom node: the leaf bodies 2i, 2i + 1
                 const uint32_t j0 = 2u * i - n;
@@ -1910,13 +1970,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
 // compiles spill-free there): when the wave's block (one frame
 // of its job's 8x8 tile) is used up, every lane computes its own pixel's primary ray for the next frame at
-// once into the wave's slice of `blk` (two float4 per lane), and lanes that need a sample read theirs.
+// once into the wave's slice of `blk` (7 floats per lane: o, d, seed; a ragged edge tile's missing pixels get d = 0,
+// which no primary ray has — 28 B instead of two float4 per lane leaves room for 90 more heap-top nodes), and lanes
+// that need a sample read theirs.
 struct BlockState {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
 };
 
 template <int MODE, bool STEAL>
-__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float4* blk, bool& drained,
+__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk, bool& drained,
                                                  uint32_t lane, unsigned long long below, bool& have,
                                                  uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
                                                  uint32_t& bounce, uint32_t& pix, uint32_t& fl) {
@@ -1950,8 +2012,14 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
                 pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
             }
-            blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
-            blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
+            float* const e = blk + 7u * threadIdx.x;
+            e[0] = pr.o.x;
+            e[1] = pr.o.y;
+            e[2] = pr.o.z;
+            e[3] = pr.d.x;
+            e[4] = pr.d.y;
+            e[5] = pr.d.z;
+            e[6] = __uint_as_float(ps);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1959,15 +2027,16 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
         const uint32_t avail = 64u - B.blk_next;
         const uint32_t rank = (uint32_t)__popcll(m & below);
         const uint32_t src = (B.blk_next + rank) & 63u;
-        const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + src)];
-        const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + src) + 1];
+        const float* const e = blk + 7u * ((threadIdx.x & ~63u) + src);
+        const float ox = e[0], oy = e[1], oz = e[2], dx = e[3], dy = e[4], dz = e[5];
+        const uint32_t es = __float_as_uint(e[6]);
         bool took = false;
         if (need && rank < avail) {
             need = false;
-            if (__float_as_uint(b1.w)) {
-                ray.o = mk(b0.x, b0.y, b0.z);
-                ray.d = mk(b0.w, b1.x, b1.y);
-                s = __float_as_uint(b1.z);
+            if (dx != 0.0f || dy != 0.0f || dz != 0.0f) {  // (a pixel outside the image: d = 0)
+                ray.o = mk(ox, oy, oz);
+                ray.d = mk(dx, dy, dz);
+                s = es;
                 fl = sample_ref(J, B.job_f0, B.blk_f);
                 pix = B.job_tile * 64u + src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
@@ -2238,30 +2307,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // HL: the heap's top in LDS (renderer.cpp decides: rt_params.heap_lds not 1 (off), and with the culling BVH a
 // sphere tree of depth <= 8, whose walk fits the 8-entry stack). 0: none, 256-lane workgroups, a 16-entry leaf-pair
 // list per lane; 1, 3: an 8-entry leaf-pair list (32-bit entries: j0 | PAIR_BIT) that shares its words with the
-// 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves per SIMD: 3 = nodes 1..991 (almost 10
-// levels, 31 KB) with 768-lane workgroups (two per CU: 78 KB each), the default; 1 = nodes 1..255 (8 levels, 8 KB)
-// with 256-lane workgroups, only for the mixed program's deferred sphere scan (its candidate lists assume 256 lanes).
-// (Nodes 1..511 with 512-lane workgroups, measured between the two in round 3, was retired.)
+// 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves per SIMD: 3 = nodes 1..1023 (7-entry list,
+// linear sphere scans) or 1..970 (culling-BVH sphere walk: 9 levels and 459 of the tenth) of sign-ordered 36-B nodes
+// (1..991 in the 32-B layout before; 881 / 971 nodes: C4 11.77 / 12.09 Grays/s) with 768-lane workgroups (two per CU:
+// 80 KB each), the default; 1 = nodes 1..255 (9 KB) with 256-lane workgroups, only for the mixed program's
+// deferred sphere scan (its candidate lists assume 256 lanes). (Nodes 1..511 with 512-lane workgroups, measured
+// between the two in round 3, was retired.)
 constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
-constexpr uint32_t heap_top_n(int hl) { return hl == 0 ? 0u : hl == 1 ? 256u : 992u; }
+// HL3 with a linear sphere scan (no sphere-walk stack in the list words): a 7-entry list, and the 3 KB it frees hold
+// the whole heap of a tree of up to 1024 nodes (Suzanne: nodes 1..1023), so the walk reads nothing but LDS (FULL)
+constexpr uint32_t heap_list_words(int hl, int scan) { return hl == 0 ? TRI_BATCH : (hl == 3 && scan != SCAN_BVH) ? 7u : 8u; }
+constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : scan != SCAN_BVH ? 1024u : 971u; }
 
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
     static_assert(MODE != MODE_SPHERE, "k_trace_split covers the sphere program");
-    constexpr uint32_t WGT = heap_wg(HL), HT = heap_top_n(HL);
+    constexpr uint32_t WGT = heap_wg(HL), HT = heap_top_n(HL, SCAN);
     const uint32_t lane = threadIdx.x & 63u;
     // per-lane deferred-triangle list (leaf-pair entries); with the culling BVH also the sphere walk's stack (never
     // live together: the sphere scan finishes in the begin phase)
-    constexpr uint32_t LIST_WORDS = HL > 0 ? TRI_BATCH / 2 : TRI_BATCH;
+    constexpr uint32_t LIST_WORDS = heap_list_words(HL, SCAN);
     constexpr int SPHERE_STACK = (int)LIST_WORDS;
+    static_assert(SCAN != SCAN_BVH || HL == 0 || LIST_WORDS == 8, "the culling walk's stack needs 8 entries");
     __shared__ uint32_t lane_words[LIST_WORDS * WGT];
     uint32_t* const cand = lane_words + threadIdx.x;  // entry k at cand[k * WGT]: a lane's entries stay in its own words
     uint32_t* const sstack = lane_words + threadIdx.x;
-    __shared__ float4 heap_top[HL > 0 ? 2 * HT : 1];
+    __shared__ float heap_top[HL > 0 ? 9 * HT : 1];  // sign-ordered nodes 0 .. HT - 1 (node_hit_so)
     if constexpr (HL > 0) {
-        const uint32_t nn = 2u * min(P.n, HT);
-        for (uint32_t t = threadIdx.x; t < nn; t += WGT) heap_top[t] = P.nodes[t];
+        const uint32_t nf = 9u * min(P.n, HT);
+        for (uint32_t t = threadIdx.x; t < nf; t += WGT) heap_top[t] = P.nodes_so[t];
         __syncthreads();
     }
     uint16_t* defer_list = nullptr;
@@ -2275,7 +2350,7 @@ k_trace_split_tris(const KParams P) {
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
-    __shared__ float4 blk[2 * WGT];  // the wave's frame block (refill_block_lds)
+    __shared__ float blk[7 * WGT];  // the wave's frame block (refill_block_lds)
     BlockState B;
     __shared__ uint32_t wjobs[(WGT / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
@@ -2322,7 +2397,23 @@ k_trace_split_tris(const KParams P) {
         if (have && qs == 3u) {
             // (triangles through a buffer descriptor: C4 +0.7 %; the culling-BVH mixed kernel makes room for it by reading
             // its sphere walk's rare-path constants through kargs(): C5 +1.2 %)
-            if (heap_run<true, HT, WGT, LIST_WORDS, true>(P, ray, W, tally, cand, suspend_below, heap_top)) qs = 4u;
+            bool walked;
+            if constexpr (HL > 0) {
+                // the sign-ordered node test unless a walking lane has a non-finite 1/d or origin (node_hit_so)
+                const bool fin3 = __builtin_isfinite(W.inv.x) && __builtin_isfinite(W.inv.y) && __builtin_isfinite(W.inv.z) &&
+                                  __builtin_isfinite(ray.o.x) && __builtin_isfinite(ray.o.y) && __builtin_isfinite(ray.o.z);
+                constexpr bool CAN_FULL = HT >= 1024u;
+                if (P.so_ok && __ballot(!fin3) == 0ull) {
+                    if (CAN_FULL && P.n <= HT)
+                        walked = heap_run<true, HT, WGT, LIST_WORDS, true, true, CAN_FULL>(P, ray, W, tally, cand, suspend_below, heap_top);
+                    else
+                        walked = heap_run<true, HT, WGT, LIST_WORDS, true, true>(P, ray, W, tally, cand, suspend_below, heap_top);
+                } else
+                    walked = heap_run<true, HT, WGT, LIST_WORDS, true, false>(P, ray, W, tally, cand, suspend_below, heap_top);
+            } else {
+                walked = heap_run<true, HT, WGT, LIST_WORDS, true>(P, ray, W, tally, cand, suspend_below);
+            }
+            if (walked) qs = 4u;
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 4u);
@@ -2367,9 +2458,10 @@ k_trace_split_tris(const KParams P) {
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
     if (lane == 0) {
+        unsigned long long* const cnt = kargs()->counter;  // (loaded here, not held in SGPRs across the kernel)
 #pragma unroll
         for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
+            if (sums[c]) atomicAdd(cnt + c, sums[c]);
     }
 }
 
