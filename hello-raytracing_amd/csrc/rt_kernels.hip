@@ -1970,18 +1970,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
 // compiles spill-free there): when the wave's block (one frame
 // of its job's 8x8 tile) is used up, every lane computes its own pixel's primary ray for the next frame at
-// once into the wave's slice of `blk` (7 floats per lane: o, d, seed; a ragged edge tile's missing pixels get d = 0,
-// which no primary ray has — 28 B instead of two float4 per lane leaves room for 90 more heap-top nodes), and lanes
-// that need a sample read theirs.
+// once into the wave's slice of `blk` (o, d and, SEED, the RNG state after the primary ray: 7 floats per lane; a ragged
+// edge tile's missing pixels get d = 0, which no primary ray has), and lanes that need a sample read theirs. Without
+// SEED (6 floats per lane) a taken sample's RNG state is recomputed from its pixel: it starts at (x * H + y) * time
+// (primary_ray) = the row's (x0 * H + y) * time + (x - x0) * H * time, per-row words in `rows` (9 per wave), then
+// five PCG steps. (Two float4 per lane before round 4: the bytes saved hold the whole heap top.)
 struct BlockState {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
 };
 
-template <int MODE, bool STEAL>
-__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk, bool& drained,
+template <int MODE, bool STEAL, bool SEED>
+__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
+                                                 uint32_t* rows, bool& drained,
                                                  uint32_t lane, unsigned long long below, bool& have,
                                                  uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
                                                  uint32_t& bounce, uint32_t& pix, uint32_t& fl) {
+    constexpr uint32_t BW = SEED ? 7u : 6u;  // floats per frame-block entry
     bool need = !have && !drained;
     unsigned long long m = __ballot(need);
     while (m != 0ull) {
@@ -2008,18 +2012,23 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             const uint32_t pok = (x < K->W && kr < K->nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
             uint32_t ps = 0;
-            if (pok) {
-                const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
-                pr = primary_ray<MODE>(&kargs()->cam, x, y, K->time0 + (B.job_f0 + B.blk_f) * K->dtime, ps);
-            }
-            float* const e = blk + 7u * threadIdx.x;
+            const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
+            const uint32_t time = K->time0 + (B.job_f0 + B.blk_f) * K->dtime;
+            if (pok) pr = primary_ray<MODE>(&kargs()->cam, x, y, time, ps);
+            float* const e = blk + BW * threadIdx.x;
             e[0] = pr.o.x;
             e[1] = pr.o.y;
             e[2] = pr.o.z;
             e[3] = pr.d.x;
             e[4] = pr.d.y;
             e[5] = pr.d.z;
-            e[6] = __uint_as_float(ps);
+            if constexpr (SEED) {
+                e[6] = __uint_as_float(ps);
+            } else {
+                uint32_t* const rw = rows + 9u * (threadIdx.x >> 6);
+                if ((lane & 7u) == 0u) rw[lane >> 3] = (x * K->cam.H + y) * time;  // the row's state seed at x0
+                if (lane == 0u) rw[8] = K->cam.H * time;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2027,16 +2036,23 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
         const uint32_t avail = 64u - B.blk_next;
         const uint32_t rank = (uint32_t)__popcll(m & below);
         const uint32_t src = (B.blk_next + rank) & 63u;
-        const float* const e = blk + 7u * ((threadIdx.x & ~63u) + src);
+        const float* const e = blk + BW * ((threadIdx.x & ~63u) + src);
         const float ox = e[0], oy = e[1], oz = e[2], dx = e[3], dy = e[4], dz = e[5];
-        const uint32_t es = __float_as_uint(e[6]);
         bool took = false;
         if (need && rank < avail) {
             need = false;
             if (dx != 0.0f || dy != 0.0f || dz != 0.0f) {  // (a pixel outside the image: d = 0)
                 ray.o = mk(ox, oy, oz);
                 ray.d = mk(dx, dy, dz);
-                s = es;
+                if constexpr (SEED) {
+                    s = __float_as_uint(e[6]);
+                } else {
+                    const uint32_t* const rw = rows + 9u * (threadIdx.x >> 6);
+                    uint32_t st = rw[src >> 3] + (src & 7u) * rw[8];
+#pragma unroll
+                    for (int k = 0; k < 5; k++) st = pcg_next(st);  // primary_ray's five draws (r1, r2, q1, q2, rr)
+                    s = st;
+                }
                 fl = sample_ref(J, B.job_f0, B.blk_f);
                 pix = B.job_tile * 64u + src;
                 sky_t = ray.d.y * 0.5f + 0.5f;
@@ -2307,17 +2323,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // HL: the heap's top in LDS (renderer.cpp decides: rt_params.heap_lds not 1 (off), and with the culling BVH a
 // sphere tree of depth <= 8, whose walk fits the 8-entry stack). 0: none, 256-lane workgroups, a 16-entry leaf-pair
 // list per lane; 1, 3: an 8-entry leaf-pair list (32-bit entries: j0 | PAIR_BIT) that shares its words with the
-// 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves per SIMD: 3 = nodes 1..1023 (7-entry list,
-// linear sphere scans) or 1..970 (culling-BVH sphere walk: 9 levels and 459 of the tenth) of sign-ordered 36-B nodes
-// (1..991 in the 32-B layout before; 881 / 971 nodes: C4 11.77 / 12.09 Grays/s) with 768-lane workgroups (two per CU:
-// 80 KB each), the default; 1 = nodes 1..255 (9 KB) with 256-lane workgroups, only for the mixed program's
+// 8-entry sphere-walk stack, which makes room for the heap's top at 6 waves per SIMD: 3 = nodes 1..1023 of sign-ordered
+// 36-B nodes, the whole heap of a tree of up to 1024 nodes (Suzanne), with 768-lane workgroups (two per CU: 80 KB
+// each), the default (1..991 in the 32-B layout before; 881 / 971 / 1023 nodes: C4 11.77 / 12.09 / 12.74 Grays/s); 1 = nodes 1..255 (9 KB) with 256-lane workgroups, only for the mixed program's
 // deferred sphere scan (its candidate lists assume 256 lanes). (Nodes 1..511 with 512-lane workgroups, measured
 // between the two in round 3, was retired.)
 constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
-// HL3 with a linear sphere scan (no sphere-walk stack in the list words): a 7-entry list, and the 3 KB it frees hold
-// the whole heap of a tree of up to 1024 nodes (Suzanne: nodes 1..1023), so the walk reads nothing but LDS (FULL)
+// Every HL3 kernel holds the whole heap of a tree of up to 1024 nodes (Suzanne: nodes 1..1023) in LDS, so the walk
+// reads nothing but LDS (FULL): the linear sphere scans (no sphere-walk stack in the list words) with a 7-entry list,
+// the culling-BVH sphere walk (8-entry stack) with 24-B frame-block entries (refill_block_lds)
 constexpr uint32_t heap_list_words(int hl, int scan) { return hl == 0 ? TRI_BATCH : (hl == 3 && scan != SCAN_BVH) ? 7u : 8u; }
-constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : scan != SCAN_BVH ? 1024u : 971u; }
+constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : 1024u; }
 
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
@@ -2350,7 +2366,11 @@ k_trace_split_tris(const KParams P) {
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
-    __shared__ float blk[7 * WGT];  // the wave's frame block (refill_block_lds)
+    // the wave's frame block (refill_block_lds): the seed stored (7 floats per lane) unless the culling-BVH sphere walk's
+    // 8-entry stack needs the list words (6 floats per lane, the seed recomputed: C5 +4.6 %, C4 -1.4 %)
+    constexpr bool SEED = !(HL == 3 && SCAN == SCAN_BVH);
+    __shared__ float blk[(SEED ? 7 : 6) * WGT];
+    __shared__ uint32_t blk_rows[SEED ? 1 : 9 * (WGT / 64u)];
     BlockState B;
     __shared__ uint32_t wjobs[(WGT / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
@@ -2366,7 +2386,8 @@ k_trace_split_tris(const KParams P) {
     HeapWalk W;
     HRT_PHASE_DECL;
     while (true) {
-        refill_block_lds<MODE, STEAL>(P, B, J, blk, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix, fl);
+        refill_block_lds<MODE, STEAL, SEED>(P, B, J, blk, blk_rows, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix,
+                                      fl);
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
@@ -2404,7 +2425,7 @@ k_trace_split_tris(const KParams P) {
                                   __builtin_isfinite(ray.o.x) && __builtin_isfinite(ray.o.y) && __builtin_isfinite(ray.o.z);
                 constexpr bool CAN_FULL = HT >= 1024u;
                 if (P.so_ok && __ballot(!fin3) == 0ull) {
-                    if (CAN_FULL && P.n <= HT)
+                    if (CAN_FULL && kargs()->n <= HT)  // (a fresh scalar load: the flag held in SGPRs spilled)
                         walked = heap_run<true, HT, WGT, LIST_WORDS, true, true, CAN_FULL>(P, ray, W, tally, cand, suspend_below, heap_top);
                     else
                         walked = heap_run<true, HT, WGT, LIST_WORDS, true, true>(P, ray, W, tally, cand, suspend_below, heap_top);
