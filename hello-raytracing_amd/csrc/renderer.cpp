@@ -306,9 +306,10 @@ std::vector<uint4> pack_bvh_hnodes(const std::vector<hrt::SphereBvhNode>& nodes,
         const float* mx[2] = {n.lmax, n.rmax};
         const uint32_t w[2] = {n.left, n.right};
         for (int c = 0; c < 2; c++) {
-            out[2 * j + c] = uint4{rel(mn[c][0], 0, false) | rel(mn[c][1], 1, false) << 16,
-                                   rel(mn[c][2], 2, false) | rel(mx[c][0], 0, true) << 16,
-                                   rel(mx[c][1], 1, true) | rel(mx[c][2], 2, true) << 16, w[c]};
+            // per axis one [min | max] pair of halves (k_trace_split rotates a pair to [near | far]: box_hit_so)
+            out[2 * j + c] = uint4{rel(mn[c][0], 0, false) | rel(mx[c][0], 0, true) << 16,
+                                   rel(mn[c][1], 1, false) | rel(mx[c][1], 1, true) << 16,
+                                   rel(mn[c][2], 2, false) | rel(mx[c][2], 2, true) << 16, w[c]};
         }
     }
     return out;

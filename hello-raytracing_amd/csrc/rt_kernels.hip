@@ -265,7 +265,9 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 }
 
 // Returns true when the walk has to run (false: bvh_end does the full scan).
-template <bool H16 = false, bool FAST = false, bool KA = false>
+// SO (k_trace_split's sign-ordered box test, box_hit_so): Q.S.lo / hi hold the near / far plane constants instead of
+// the min / max ones (swapped per axis where 1/d < 0).
+template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -304,6 +306,11 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     Q.S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
     Q.S.lo = Q.S.lo * Q.S.inv;
     Q.S.hi = Q.S.hi * Q.S.inv;
+    if constexpr (SO) {
+        const f3 lo = Q.S.lo, hi = Q.S.hi;
+        Q.S.lo = mk(Q.S.inv.x < 0.0f ? hi.x : lo.x, Q.S.inv.y < 0.0f ? hi.y : lo.y, Q.S.inv.z < 0.0f ? hi.z : lo.z);
+        Q.S.hi = mk(Q.S.inv.x < 0.0f ? lo.x : hi.x, Q.S.inv.y < 0.0f ? lo.y : hi.y, Q.S.inv.z < 0.0f ? lo.z : hi.z);
+    }
     Q.node = P.bvh_root;
     return true;
 }
@@ -315,26 +322,50 @@ typedef _Float16 hrt_h2 __attribute__((ext_vector_type(2)));
 // (v_fma_mix_f32: the f16 operand is widened exactly inside the f32 FMA, no conversions).
 __device__ __forceinline__ float h16_lo(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).x; }
 __device__ __forceinline__ float h16_hi(uint32_t u) { return (float)__builtin_bit_cast(hrt_h2, u).y; }
-// a node with fp16 boxes (2 uint4) as the 4 float4 of the f32 layout: lmin|left, lmax, rmin|right, rmax
+// a node with fp16 boxes (2 uint4: per child [min|max] halves of x, y, z and the child word; renderer.cpp
+// pack_bvh_hnodes) as the 4 float4 of the f32 layout: lmin|left, lmax, rmin|right, rmax
 __device__ __forceinline__ void load_hnode(const uint4* __restrict__ hn, uint32_t node, float4& n0, float4& n1,
                                            float4& n2, float4& n3) {
     const uint4 c0 = hn[2 * node], c1 = hn[2 * node + 1];
-    n0 = float4{h16_lo(c0.x), h16_hi(c0.x), h16_lo(c0.y), __uint_as_float(c0.w)};
-    n1 = float4{h16_hi(c0.y), h16_lo(c0.z), h16_hi(c0.z), 0.0f};
-    n2 = float4{h16_lo(c1.x), h16_hi(c1.x), h16_lo(c1.y), __uint_as_float(c1.w)};
-    n3 = float4{h16_hi(c1.y), h16_lo(c1.z), h16_hi(c1.z), 0.0f};
+    n0 = float4{h16_lo(c0.x), h16_lo(c0.y), h16_lo(c0.z), __uint_as_float(c0.w)};
+    n1 = float4{h16_hi(c0.x), h16_hi(c0.y), h16_hi(c0.z), 0.0f};
+    n2 = float4{h16_lo(c1.x), h16_lo(c1.y), h16_lo(c1.z), __uint_as_float(c1.w)};
+    n3 = float4{h16_hi(c1.x), h16_hi(c1.y), h16_hi(c1.z), 0.0f};
+}
+
+// Sign-ordered padded box test (k_trace_split; the nodes' [min|max] fp16 pairs): each pair rotated by 16 bits where
+// 1/d < 0 (sh = 16) puts the near plane in the low half, so with the near / far constants of bvh_begin<.., SO> the
+// planes' t values are those of padded_box_hit_nb — one FMA per plane, the same roundings — and near <= far without a
+// min / max per axis (min <= max, a bound and its constant order the same way, FMA rounding is monotone; 1/d is never
+// 0 or NaN: robust_inv). One rotate per axis replaces a min and a max: the same visits, bit for bit.
+__device__ __forceinline__ bool box_hit_so(uint32_t px, uint32_t py, uint32_t pz, uint32_t shx, uint32_t shy, uint32_t shz,
+                                           const Slab& S, float bt, float& tenter) {
+    const uint32_t x = __builtin_amdgcn_alignbit(px, px, shx), y = __builtin_amdgcn_alignbit(py, py, shy),
+                   z = __builtin_amdgcn_alignbit(pz, pz, shz);
+    const float tnx = __builtin_fmaf(h16_lo(x), S.inv.x, S.lo.x), tfx = __builtin_fmaf(h16_hi(x), S.inv.x, S.hi.x);
+    const float tny = __builtin_fmaf(h16_lo(y), S.inv.y, S.lo.y), tfy = __builtin_fmaf(h16_hi(y), S.inv.y, S.hi.y);
+    const float tnz = __builtin_fmaf(h16_lo(z), S.inv.z, S.lo.z), tfz = __builtin_fmaf(h16_hi(z), S.inv.z, S.hi.z);
+    const float tmin = fmax_ieee(fmax_ieee(tnx, tny), fmax_ieee(tnz, 0.0f));
+    const float tmax = fmin_ieee(fmin_ieee(tfx, tfy), tfz);
+    tenter = tmin;
+    return tmin <= tmax && tmin <= bt;
 }
 
 // NOOVF: the stack cannot overflow — a tree of depth <= STACK (renderer.cpp gates k_trace_split<LNODES> and the
 // mixed kernels' 8-entry stack on depth <= 8): visiting a node of depth d the stack holds at most d entries (one
 // pending sibling per level above it), so a push at an internal node (d <= depth - 1) leaves at most depth. The
 // push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
+// SO (with SELECT and H16; Q from bvh_begin<.., SO>): box_hit_so.
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
-          bool NOOVF = false>
+          bool NOOVF = false, bool SO = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
+    static_assert(!SO || (SELECT && H16), "the sign-ordered box test reads fp16 pairs in the select-form walk");
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
+    // SO: the rotation of each axis pair, 16 where 1/d < 0 (recomputed per call: not kept across rounds)
+    const uint32_t shx = SO ? (__float_as_uint(S.inv.x) >> 27) & 16u : 0u, shy = SO ? (__float_as_uint(S.inv.y) >> 27) & 16u : 0u,
+                   shz = SO ? (__float_as_uint(S.inv.z) >> 27) & 16u : 0u;
     const float a = dot(r.d, r.d);  // the same value bvh_begin computed
     const float a4 = 4.0f * a, a2 = 2.0f * a;
     uint32_t node = Q.node;
@@ -352,23 +383,34 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 if (first_active_lane()) tally.wbox++;
             }
 #endif
-            float4 n0, n1, n2, n3;
-            if constexpr (H16) {
-                load_hnode(hn, node, n0, n1, n2, n3);
-            } else {
-                n0 = nodes[4 * node + 0];
-                n1 = nodes[4 * node + 1];
-                n2 = nodes[4 * node + 2];
-                n3 = nodes[4 * node + 3];
-            }
             float tl, tr;
-            // SELECT (k_trace_split): best-t bound as a separate compare (no per-step canonicalize of bt)
-            // and select-form child order, +1 % on C3; the three-way branch below keeps k_trace's mixed
-            // program (C5) free of spills (the select form spilled 12 VGPRs there, -1.5 %).
-            const bool hl = SELECT ? padded_box_hit_nb(n0, n1, S, bt, tl) : padded_box_hit(n0, n1, S, bt, tl);
-            const bool hr = SELECT ? padded_box_hit_nb(n2, n3, S, bt, tr) : padded_box_hit(n2, n3, S, bt, tr);
+            bool hl, hr;
+            uint32_t left, right;
+            if constexpr (SO) {
+                const uint4 c0 = hn[2 * node], c1 = hn[2 * node + 1];
+                hl = box_hit_so(c0.x, c0.y, c0.z, shx, shy, shz, S, bt, tl);
+                hr = box_hit_so(c1.x, c1.y, c1.z, shx, shy, shz, S, bt, tr);
+                left = c0.w;
+                right = c1.w;
+            } else {
+                float4 n0, n1, n2, n3;
+                if constexpr (H16) {
+                    load_hnode(hn, node, n0, n1, n2, n3);
+                } else {
+                    n0 = nodes[4 * node + 0];
+                    n1 = nodes[4 * node + 1];
+                    n2 = nodes[4 * node + 2];
+                    n3 = nodes[4 * node + 3];
+                }
+                // SELECT (k_trace_split): best-t bound as a separate compare (no per-step canonicalize of bt)
+                // and select-form child order, +1 % on C3; the three-way branch below keeps k_trace's mixed
+                // program (C5) free of spills (the select form spilled 12 VGPRs there, -1.5 %).
+                hl = SELECT ? padded_box_hit_nb(n0, n1, S, bt, tl) : padded_box_hit(n0, n1, S, bt, tl);
+                hr = SELECT ? padded_box_hit_nb(n2, n3, S, bt, tr) : padded_box_hit(n2, n3, S, bt, tr);
+                left = __float_as_uint(n0.w);
+                right = __float_as_uint(n2.w);
+            }
             tally.boxes += 2;
-            const uint32_t left = __float_as_uint(n0.w), right = __float_as_uint(n2.w);
             if constexpr (SELECT && NOOVF) {
                 // (updates written unconditionally: the node and stack depth stay in one register each across the
                 // descent loop instead of being copied at its head)
@@ -2233,7 +2275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(0, have && qs == 0u);
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
-                qs = bvh_begin<true, true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+                qs = bvh_begin<true, true, true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
             } else {  // bounce cap 0: the sample is the sky colour
                 qs = 3u;
             }
@@ -2242,9 +2284,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
             if constexpr (LNODES) {  // (depth <= LNODE_DEPTH = SPLIT_STACK: no overflow)
-                if (bvh_run<true, SPLIT_STACK, true, true, 256, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, true, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
             } else {
-                if (bvh_run<true, SPLIT_STACK, true, true>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, false, true>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
                     qs = 2u;
             }
         }
