@@ -355,12 +355,12 @@ __device__ __forceinline__ bool box_hit_so(uint32_t px, uint32_t py, uint32_t pz
 // mixed kernels' 8-entry stack on depth <= 8): visiting a node of depth d the stack holds at most d entries (one
 // pending sibling per level above it), so a push at an internal node (d <= depth - 1) leaves at most depth. The
 // push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
-// SO (with SELECT and H16; Q from bvh_begin<.., SO>): box_hit_so.
+// SO (with H16; Q from bvh_begin<.., SO>): box_hit_so.
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
           bool NOOVF = false, bool SO = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
-    static_assert(!SO || (SELECT && H16), "the sign-ordered box test reads fp16 pairs in the select-form walk");
+    static_assert(!SO || H16, "the sign-ordered box test reads fp16 pairs");
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
     // SO: the rotation of each axis pair, 16 where 1/d < 0 (recomputed per call: not kept across rounds)
@@ -518,12 +518,12 @@ __device__ __forceinline__ int bvh_end(const KParams& P, const Ray& r, const Bvh
     return Q.bc >= 0 ? bvh_slot_of(P, Q.bc) : -1;
 }
 
-template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256, bool KA = false, bool NOOVF = false>
+template <int STACK = BVH_STACK, bool H16 = true, uint32_t LS = 256, bool KA = false, bool NOOVF = false, bool SO = false>
 __device__ __forceinline__ int scan_spheres_bvh(const KParams& P, const Ray& r, float& best, uint32_t* stack,
                                                 Tally& tally) {
     BvhQuery Q;
-    if (bvh_begin<H16, false, KA>(P, r, best, Q, tally))
-        bvh_run<false, STACK, false, H16, LS, NOOVF>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
+    if (bvh_begin<H16, false, KA, SO>(P, r, best, Q, tally))
+        bvh_run<false, STACK, false, H16, LS, NOOVF, SO>(P, r, Q, stack, tally, 0u, P.bvh_hnodes);
     return bvh_end<KA>(P, r, Q, best, tally);
 }
 
@@ -2447,7 +2447,7 @@ k_trace_split_tris(const KParams P) {
             } else {
                 float sb = FLT_MAX_REF;
                 // (HL > 0: renderer.cpp runs these only for sphere trees of depth <= 8 = SPHERE_STACK: no overflow)
-                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true, (HL > 0)>(P, ray, sb, sstack, tally);
+                if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true, (HL > 0), true>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own

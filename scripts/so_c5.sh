@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# Sign-ordered culling-BVH box test in the mixed kernel's sphere walk too (lib/libhrt.so) against the previous commit
+# (lib/libhrt_base.so): the GPU suite, then C5 at 256 spp (two rounds) and at 4096 spp.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+o=gpurun_out/so_c5
+mkdir -p $o
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $o/gputest.log 2>&1 || { tail -30 $o/gputest.log; exit 1; }
+tail -1 $o/gputest.log
+run() {  # lib cfg tag steps [extra]
+  HRT_LIB=$1 timeout -k 10 300 python bench.py --config $2 --steps $4 --warmup 1 --emulate-ranks 0 --no-cpu-baseline \
+    --no-golden $5 > $o/$2_$3.log 2>&1 || return $?
+  echo "$3 $2 $1 $(tail -1 $o/$2_$3.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+}
+for round in 1 2; do
+  run lib/libhrt_base.so c5 base$round 1 "--frames 256" && run lib/libhrt.so c5 so$round 1 "--frames 256" || exit 1
+done
+run lib/libhrt_base.so c5 basefull 1 && run lib/libhrt.so c5 sofull 1
