@@ -575,11 +575,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         jf = 1u << P.jf_log2;
         // How the colours are folded (rt_params.queue_budget_mb, fold): the sample buffer (every colour
         // of a launch, then k_accumulate) in launches of equal frame counts, or the bounded-memory fold ring.
-        //   queue_budget_mb 0 (auto, the default): floor(count / 320) launches (at least one). A launch of 320+ frames
-        //     loses ~2 % to one launch of every frame (C3 3 x 342 frames: 33.8 vs 34.5 Grays/s), shorter ones lose more
-        //     (fewer jobs per tile spread the waves over more of the image; C3 at 82 / 164 frames 29.3 / 31.5, C4 in
-        //     launches of 345 + 167 frames -13 %), so the buffer holds at most 639 frames (C3: 8.5 GB, not 25.5), and at
-        //     most AUTO_BUDGET;
+        //   queue_budget_mb 0 (auto, the default): floor(count / 320) launches (at least one) of whole jobs. A launch of
+        //     320+ frames loses ~2 % to one launch of every frame (C3 3 x 342 frames: 33.8 vs 34.5 Grays/s), shorter ones
+        //     lose more (fewer jobs per tile spread the waves over more of the image; C3 at 82 / 164 frames 29.3 / 31.5,
+        //     C4 in launches of 345 + 167 frames -13 %), so the buffer holds at most ~640 frames (C3: 8.8 GB, not 25.5),
+        //     and at most AUTO_BUDGET;
         //   queue_budget_mb > 0: a cap in MiB, launches of as many frames as it holds, balanced;
         //   the fold ring (fold 0) when a launch would get fewer than min(count, 320) frames.
         // (Pipelined launches of tile-row bands x every frame, which keep every frame of a tile in one launch within a
@@ -590,15 +590,19 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         const size_t frame_bytes = frame_floats * 4u;
         const uint32_t nframes_all = std::max(count, 1u);
         size_t budget = (size_t)r->params.queue_budget_mb << 20;
-        if (r->params.queue_budget_mb == 0u) {
-            const uint32_t n = std::max(1u, nframes_all / 320u);
-            budget = std::min(AUTO_BUDGET, (size_t)((nframes_all + n - 1u) / n) * frame_bytes);
-        }
-        auto balanced = [&](size_t fit) {  // equal launches of at most `fit` frames
+        // equal launches of at most `fit` frames, rounded up to whole jobs where that still fits: every launch but the
+        // last then holds whole jobs, so the tail split applies (C3: 352 + 352 + 320 frames, not 3 x 342)
+        auto balanced = [&](size_t fit) {
             fit = std::max<size_t>(1, std::min<size_t>(fit, nframes_all));
             const size_t n = (nframes_all + fit - 1u) / fit;
-            return (uint32_t)((nframes_all + n - 1u) / n);
+            const size_t c = (nframes_all + n - 1u) / n, cj = (c + jf - 1u) / jf * jf;
+            return (uint32_t)(cj <= fit ? cj : c);
         };
+        if (r->params.queue_budget_mb == 0u) {
+            const uint32_t n = std::max(1u, nframes_all / 320u);
+            const size_t c = (nframes_all + n - 1u) / n, cj = (c + jf - 1u) / jf * jf;
+            budget = std::min(AUTO_BUDGET, std::min<size_t>(cj, nframes_all) * frame_bytes);
+        }
         uint32_t chunk = balanced(budget / frame_bytes), log2s = 0;
         P.ring_mode = chunk < std::min(nframes_all, 320u) ? 1u : 0u;
         if (r->params.fold == RT_FOLD_BUFFER) P.ring_mode = 0u;  // forced (measurements, tests)

@@ -179,13 +179,13 @@ def test_sample_queue_chunks_and_tris_mode():
         assert (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), st.fold_bytes
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 320 MiB hold 364 frames (>= 320: the sample buffer)
-    # -> 700 frames in two balanced launches of 350; the default budget (auto: floor(700 / 320) = 2 launches) the
-    # same; 1000 MiB hold all 700 frames: one launch
+    # -> 700 frames in two balanced launches of whole jobs, 352 + 348; the default budget (auto: floor(700 / 320) = 2
+    # launches) the same; 1000 MiB hold all 700 frames: one launch
     per_frame = 1200 * 64 * 12
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
     ref.draw_frames(700, 1000, 10)
-    for mb, nl, chunk in ((320, 2, 350), (None, 2, 350), (1000, 1, 700)):
+    for mb, nl, chunk in ((320, 2, 352), (None, 2, 352), (1000, 1, 700)):
         r = scenes.make_renderer(sd)
         r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **({"queue_budget_mb": mb} if mb else {}))
         r.draw_frames(700, 1000, 10)
