@@ -691,16 +691,17 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                                   (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
                 P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
             }
-            // Tail split (k_trace_split with the sample buffer, no stealing): the last ~2 jobs per resident wave
-            // are dealt as quarter jobs, so the launch's drain waits for a quarter job, not a whole one (job_frames
-            // a multiple of 4 and whole chunks only; rt_params.tail_split = 1 turns it off)
+            // Tail split (the suspendable-walk kernels with the sample buffer, no stealing): the last ~2 jobs per
+            // resident wave are dealt in parts (rt_params.tail_split: 2 quarters, 3 eighths; 0 auto = quarters),
+            // so the launch's drain waits for a part, not a whole job (job_frames a multiple of the part count and
+            // whole chunks only; tail_split 1 turns it off)
             P.tail_from = 0xFFFFFFFFu;
-            const bool sphere_split = r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_BVH && P.suspend_below > 0u;
-            if (sphere_split && !P.ring_mode && !P.steal && P.job_frames % 4u == 0u && P.nframes % P.job_frames == 0u &&
-                r->params.tail_split != 1u && P.njobs < (1ull << 30)) {
+            P.tail_shift = r->params.tail_split == 3u ? 3u : 2u;
+            if (split && P.suspend_below > 0u && !P.ring_mode && !P.steal && P.job_frames % (1u << P.tail_shift) == 0u &&
+                P.nframes % P.job_frames == 0u && r->params.tail_split != 1u && P.njobs < (1ull << 29)) {
                 const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
                 P.tail_from = (uint32_t)(P.njobs - q);
-                P.njobs += 3ull * q;
+                P.njobs += ((1ull << P.tail_shift) - 1u) * q;
             }
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
@@ -939,7 +940,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
     if (p->heap_lds > 2) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2 on");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
-    if (p->tail_split > 1) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto or 1 off");
+    if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

@@ -158,7 +158,8 @@ struct KParams {
     uint32_t jf_log2, pad_r;      // job_frames = 1 << jf_log2
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames), + 3 per job split in quarters
-    uint32_t tail_from, pad_t;    // sample buffer: jobs from this index on are quarter jobs (4 per original job)
+    uint32_t tail_from;           // sample buffer: jobs from this index on are parts of jobs (2^tail_shift per job)
+    uint32_t tail_shift;
     uint32_t tiles_w, tiles_h;    // 8x8 tiles over W x nrows
     uint32_t job_frames, nchunks; // frames per job (a job = one tile x job_frames frames), chunks per tile
     uint32_t suspend_below;       // k_trace_split: suspend the walks once fewer lanes than this still walk

@@ -1394,18 +1394,19 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
         }
         J.set(WJ_FLAGS, flags | WJ_DEALING);
         if constexpr (TAIL) {
-            // The launch's last jobs are dealt in quarters: a job dealt late then ends soon after the queue
-            // drains instead of holding the launch for a whole job (whole chunks of a job_frames multiple of 4)
-            const uint32_t tail = K->tail_from;
-            const bool quarter = j >= tail;
+            // The launch's last jobs are dealt in parts (2^tail_shift per job): a job dealt late then ends soon after
+            // the queue drains instead of holding the launch for a whole job (whole chunks of a job_frames multiple of
+            // the part count)
+            const uint32_t tail = K->tail_from, ts = K->tail_shift;
+            const bool part = j >= tail;
             const uint32_t q = j - tail;
-            const uint32_t jj = quarter ? tail + (q >> 2) : j;
+            const uint32_t jj = part ? tail + (q >> ts) : j;
             job_tile = jj / K->nchunks;
             job_f0 = (jj - job_tile * K->nchunks) * K->job_frames;
             job_nf = min(K->job_frames, K->nframes - job_f0);
-            if (quarter) {
-                job_nf >>= 2;
-                job_f0 += (q & 3u) * job_nf;
+            if (part) {
+                job_nf >>= ts;
+                job_f0 += (q & ((1u << ts) - 1u)) * job_nf;
             }
         } else {
             job_tile = j / K->nchunks;
@@ -2044,7 +2045,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 if (J.dealing()) {
                     B.blk_f++;
                 } else {
-                    if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
+                    if (!job_acquire<true>(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                     B.blk_f = 0;
                 }
             }
@@ -2706,9 +2707,10 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
 
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {
     if (P.njobs == 0) return hipSuccess;
-    // quarter jobs (tail_from) are decoded by k_trace_split only (job_acquire<TAIL>)
-    if (P.tail_from != 0xFFFFFFFFu && !(mode == MODE_SPHERE && variant == SCAN_BVH && P.suspend_below > 0u && !P.steal))
-        return hipErrorInvalidValue;
+    // parts of jobs (tail_from) are decoded by the suspendable-walk kernels with the sample buffer and no stealing only
+    // (job_acquire<TAIL>): k_trace_split and k_trace_split_tris (not the opt-in SAH walk's k_trace)
+    const bool split_kernel = mode == MODE_SPHERE ? (variant == SCAN_BVH && P.suspend_below > 0u) : !P.tri_bvh;
+    if (P.tail_from != 0xFFFFFFFFu && !(split_kernel && !P.steal && !P.ring_mode)) return hipErrorInvalidValue;
     switch (mode) {
     case MODE_SPHERE:
         if (variant == SCAN_BVH && P.suspend_below > 0u)

@@ -104,10 +104,11 @@ typedef struct rt_params {
                                   stealing (a wave whose job queue is drained claims single frames of other
                                   waves' jobs, so no long job trails the launch): 0 auto = on for launches of
                                   fewer than 16 jobs per resident wave, 1 off, 2 on; bit-identical always  */
-    uint32_t tail_split;       /* sphere program's culling-BVH walk (k_trace_split) with the sample buffer and no
-                                  stealing: 0 auto = the launch's last ~2 jobs per resident wave are dealt as
-                                  quarter jobs (job_frames a multiple of 4), so the drain waits for a quarter
-                                  job; 1 off; bit-identical                                              */
+    uint32_t tail_split;       /* suspendable-walk kernels (k_trace_split, k_trace_split_tris) with the sample
+                                  buffer and no stealing: the launch's last ~2 jobs per resident wave are dealt
+                                  in parts, so the drain waits for a part of a job: 0 auto (quarters), 1 off,
+                                  2 quarters, 3 eighths (job_frames a multiple of the part count);
+                                  bit-identical                                                          */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u

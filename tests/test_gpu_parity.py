@@ -544,20 +544,22 @@ def test_suspendable_heap_walk_bit_identical(variant):
 
 @pytest.mark.parametrize("jf", [4, 8, 32])
 def test_tail_split_bit_identical(jf):
-    """The launch's last jobs dealt as quarter jobs (rt_params.tail_split: k_trace_split with the sample buffer when
-    job_frames is a multiple of 4 and divides the launch's frames): images and every work count equal the draw
-    without the split and the oracle; k_trace (suspend_below 0) and the mixed program ignore the knob."""
+    """The launch's last jobs dealt in parts (rt_params.tail_split 0 auto / 2 quarters / 3 eighths: the suspendable-walk
+    kernels, k_trace_split and k_trace_split_tris, with the sample buffer when job_frames is a multiple of the part
+    count and divides the launch's frames): images and every work count equal the draw without the split (1) and the
+    oracle; the sphere program with suspend_below 0 included."""
     for sd, extra in ((scenes.config_c3(136, 80, 32), {}), (scenes.config_c3(136, 80, 32), {"suspend_below": 0}),
-                      (scenes.config_c4(120, 72, 32), {})):
+                      (scenes.config_c4(120, 72, 32), {}), (scenes.config_c5(96, 64, 32), {})):
         runs = []
-        for tail in (0, 1):
+        for tail in (1, 0, 2, 3):
             r = scenes.make_renderer(sd)
             r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, tail_split=tail, job_frames=jf, steal=1, **extra)
             r.draw_frames(sd.frames, 1000, 10)
             st = r.stats()
             runs.append((r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests, st.box_tests)))
-        np.testing.assert_array_equal(runs[0][0].view(np.uint32), runs[1][0].view(np.uint32), err_msg=sd.name)
-        assert runs[0][1] == runs[1][1], (sd.name, runs[0][1], runs[1][1])
+        for img, counts in runs[1:]:
+            np.testing.assert_array_equal(runs[0][0].view(np.uint32), img.view(np.uint32), err_msg=sd.name)
+            assert runs[0][1] == counts, (sd.name, runs[0][1], counts)
     ref, q = scenes.oracle_render(sd)
     assert_parity(runs[0][0], ref, f"{sd.name} tail split, job_frames {jf}")
     assert runs[0][1][0] == q
