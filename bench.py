@@ -404,8 +404,11 @@ def main() -> int:
         extra["steal"] = args.steal
     if args.tail_split is not None:
         extra["tail_split"] = args.tail_split
+    # the timed draws run the default kernels (count_tests 0: the sphere program's k_trace_split does not count its box
+    # and sphere tests); the warmup draws count them (count_tests 1) for the per-ray figures of the line, the same
+    # every step (bit-identical draws)
     knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
-                 tri_bvh=args.tri_bvh, **extra)
+                 tri_bvh=args.tri_bvh, count_tests=0, **extra)
     r.set_params(**rank_params(rank, world, args.row_block), **knobs)
     local_rows = r.local_rows
     part = torch.zeros((max_rows(world, sd.height, args.row_block), sd.width, 3), dtype=torch.float32, device=dev)
@@ -438,9 +441,17 @@ def main() -> int:
 
     log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
         f"{local_rows} rows, warmup {args.warmup}")
+    counted = None  # (box tests, sphere tests) of one step, from a counting draw
+
+    def counting_step():
+        r.set_params(count_tests=1)
+        st = step()
+        r.set_params(count_tests=0)
+        return st.box_tests, st.sphere_tests
+
     for i in range(args.warmup):
         t = time.perf_counter()
-        step()
+        counted = counting_step()
         torch.cuda.synchronize()
         log(f"warmup {i}: {time.perf_counter() - t:.2f} s")
 
@@ -460,6 +471,7 @@ def main() -> int:
     trace_ms = 0.0
     trace_launches = 0
     st_last = None
+    uncounted = False
     for i in range(args.steps):
         st = step()
         st_last = st
@@ -468,6 +480,7 @@ def main() -> int:
         launches += st.launches
         box_tests += st.box_tests
         sphere_tests += st.sphere_tests
+        uncounted = st.box_tests == 0 and st.sphere_tests == 0
         node_tests += st.node_tests
         tri_tests += st.tri_tests
         variant = st.variant
@@ -479,6 +492,15 @@ def main() -> int:
             f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
     barrier()
     elapsed = time.perf_counter() - t0
+    if args.steps and uncounted:  # the timed kernels did not count: the per-step counts of a counting draw
+        if counted is None:  # (no warmup: one more draw after the timed region, rank-local, no collective)
+            r.set_params(count_tests=1)
+            r.reset_frame_count()
+            r.draw_frames(sd.frames, 1000, 10)
+            st_c = r.stats()
+            r.set_params(count_tests=0)
+            counted = (st_c.box_tests, st_c.sphere_tests)
+        box_tests, sphere_tests = counted[0] * args.steps, counted[1] * args.steps
     emulated = None
     n_emul = args.emulate_ranks if args.emulate_ranks is not None else (8 if world == 1 else 0)
     if world == 1 and n_emul > 1:

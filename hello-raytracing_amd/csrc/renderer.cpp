@@ -495,6 +495,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.nodes = r->nodes.ptr;
     P.nodes_so = r->nodes_so.ptr;
     P.so_ok = r->so_ok ? 1u : 0u;
+    P.count_tests = r->params.count_tests;
     P.tris = r->tris.ptr;
     P.tri_bvh = (r->mode != RT_MODE_SPHERE && r->params.tri_bvh) ? 1u : 0u;
     if (P.tri_bvh) {
@@ -941,6 +942,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->heap_lds > 2) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2 on");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
+    if (p->count_tests > 1) return fail(RT_ERR_ARG, "rt_set_params: count_tests must be 0 or 1");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

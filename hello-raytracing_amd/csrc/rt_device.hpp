@@ -171,7 +171,8 @@ struct KParams {
     // the heap's nodes as (lo, hi, lo) per axis, 9 floats per node (renderer.cpp pack_nodes_so; the heap-top kernels'
     // sign-ordered node test, rt_kernels.hip node_hit_so); so_ok 0: a NaN bound, the reference form only
     const float* nodes_so;
-    uint32_t so_ok, pad_so;
+    uint32_t so_ok;
+    uint32_t count_tests;         // k_trace_split<.., COUNT>: box / sphere test counts (rt_params.count_tests)
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

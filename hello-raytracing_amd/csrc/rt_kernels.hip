@@ -267,7 +267,8 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
 // Returns true when the walk has to run (false: bvh_end does the full scan).
 // SO (k_trace_split's sign-ordered box test, box_hit_so): Q.S.lo / hi hold the near / far plane constants instead of
 // the min / max ones (swapped per axis where 1/d < 0).
-template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false>
+// COUNT false (k_trace_split without rt_params.count_tests): no box / sphere test counts (1.3 % of C3's kernel time).
+template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false, bool COUNT = true>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -289,7 +290,7 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
         const float t = exact_t_geo<FAST>(P.sph_geo[i], r, a4, a2);
         if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
-    tally.spheres += nlarge;
+    if constexpr (COUNT) tally.spheres += nlarge;
     Q.bt = bt;
     Q.bc = bc;
 
@@ -357,7 +358,7 @@ __device__ __forceinline__ bool box_hit_so(uint32_t px, uint32_t py, uint32_t pz
 // push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
 // SO (with H16; Q from bvh_begin<.., SO>): box_hit_so.
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
-          bool NOOVF = false, bool SO = false>
+          bool NOOVF = false, bool SO = false, bool COUNT = true>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
                                         Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
     static_assert(!SO || H16, "the sign-ordered box test reads fp16 pairs");
@@ -410,7 +411,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 left = __float_as_uint(n0.w);
                 right = __float_as_uint(n2.w);
             }
-            tally.boxes += 2;
+            if constexpr (COUNT) tally.boxes += 2;
             if constexpr (SELECT && NOOVF) {
                 // (updates written unconditionally: the node and stack depth stay in one register each across the
                 // descent loop instead of being copied at its head)
@@ -482,7 +483,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                     if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                 }
             }
-            tally.spheres += cnt;
+            if constexpr (COUNT) tally.spheres += cnt;
         }
         if (sp == 0) {
             finished = 1u;
@@ -2163,7 +2164,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
 // STEAL: frame-block work stealing (sample buffer; renderer.cpp turns it on for launches with few jobs per wave).
 // A separate instantiation: the runtime-switched form cost C3 3 % with stealing off (register allocation).
-template <bool LNODES, bool STEAL>
+template <bool LNODES, bool STEAL, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
@@ -2276,7 +2277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(0, have && qs == 0u);
         if (have && qs == 0u) {
             if (bounce < P.bounces) {
-                qs = bvh_begin<true, true, true, true>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
+                qs = bvh_begin<true, true, true, true, COUNT>(P, ray, FLT_MAX_REF, Q, tally) ? 1u : 2u;
             } else {  // bounce cap 0: the sample is the sky colour
                 qs = 3u;
             }
@@ -2285,9 +2286,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
             if constexpr (LNODES) {  // (depth <= LNODE_DEPTH = SPLIT_STACK: no overflow)
-                if (bvh_run<true, SPLIT_STACK, true, true, 256, true, true>(P, ray, Q, stack, tally, suspend_below, lnodes)) qs = 2u;
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, true, true, COUNT>(P, ray, Q, stack, tally, suspend_below, lnodes))
+                    qs = 2u;
             } else {
-                if (bvh_run<true, SPLIT_STACK, true, true, 256, false, true>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, false, true, COUNT>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
                     qs = 2u;
             }
         }
@@ -2615,8 +2617,9 @@ hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned lo
 static thread_local char g_kernel_name[64] = "";
 const char* hrt_last_kernel() { return g_kernel_name; }
 void hrt_reset_last_kernel() { g_kernel_name[0] = '\0'; }
-static const char* kname_b(const char* base, int a, int b) {  // <bool, bool>
-    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s>", base, a ? "true" : "false", b ? "true" : "false");
+static const char* kname_bbb(const char* base, int a, int b, int c) {  // <bool, bool, bool>
+    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s, %s>", base, a ? "true" : "false", b ? "true" : "false",
+             c ? "true" : "false");
     return g_kernel_name;
 }
 static const char* kname_iiib(const char* base, int a, int b, int c, int d) {  // <int, int, int, bool>
@@ -2705,6 +2708,17 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
     }
 }
 
+// k_trace_split<LNODES, STEAL, COUNT> by P.bvh_lnodes / P.steal
+template <bool COUNT>
+static hipError_t launch_trace_split(const KParams& P, hipStream_t stream) {
+    const char* base = "k_trace_split";
+    if (P.steal)
+        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT))
+                            : launch_persistent(k_trace_split<false, true, COUNT>, P, stream, kname_bbb(base, 0, 1, COUNT));
+    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT))
+                        : launch_persistent(k_trace_split<false, false, COUNT>, P, stream, kname_bbb(base, 0, 0, COUNT));
+}
+
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {
     if (P.njobs == 0) return hipSuccess;
     // parts of jobs (tail_from) are decoded by the suspendable-walk kernels with the sample buffer and no stealing only
@@ -2715,11 +2729,7 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     case MODE_SPHERE:
         if (variant == SCAN_BVH && P.suspend_below > 0u)
         {
-            if (P.steal)
-                return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true>, P, stream, kname_b("k_trace_split", 1, 1))
-                                    : launch_persistent(k_trace_split<false, true>, P, stream, kname_b("k_trace_split", 0, 1));
-            return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false>, P, stream, kname_b("k_trace_split", 1, 0))
-                                : launch_persistent(k_trace_split<false, false>, P, stream, kname_b("k_trace_split", 0, 0));
+            return P.count_tests ? launch_trace_split<true>(P, stream) : launch_trace_split<false>(P, stream);
         }
         return launch_trace_mode<MODE_SPHERE, false>(variant, P, stream);
     case MODE_TRIS:

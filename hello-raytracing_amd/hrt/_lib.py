@@ -48,6 +48,7 @@ class RtParams(C.Structure):
         ("heap_lds", C.c_uint32),
         ("steal", C.c_uint32),
         ("tail_split", C.c_uint32),
+        ("count_tests", C.c_uint32),
     ]
 
 

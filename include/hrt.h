@@ -109,6 +109,10 @@ typedef struct rt_params {
                                   in parts, so the drain waits for a part of a job: 0 auto (quarters), 1 off,
                                   2 quarters, 3 eighths (job_frames a multiple of the part count);
                                   bit-identical                                                          */
+    uint32_t count_tests;      /* 1: count the sphere program's culling-walk box and sphere tests
+                                  (rt_stats.box_tests / sphere_tests); 0 (default): the sphere program's
+                                  k_trace_split does not count them (reported 0; 1.3 % of C3's kernel
+                                  time); the other kernels always count                                  */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u

@@ -234,13 +234,12 @@ CONFIGS = {"c1": config_c1, "c2": config_c2, "c3": config_c3, "c4": config_c4, "
 def make_renderer(sd: SceneDef) -> "hrt.Renderer":
     """GPU renderer loaded with a SceneDef (camera, buffers, params)."""
     r = hrt.Renderer(sd.width, sd.height, sd.mode)
-    kw = {}
+    kw = {"count_tests": 1}  # (the tests compare work counts; bench.py turns the counting off for its timed steps)
     if sd.bounces is not None:
         kw["bounces"] = sd.bounces
     if sd.min_sphere_slots is not None:
         kw["min_sphere_slots"] = sd.min_sphere_slots
-    if kw:
-        r.set_params(**kw)
+    r.set_params(**kw)
     r.set_camera(sd.camera)
     if sd.mode != hrt.RT_MODE_TRIS:
         r.write_spheres(sd.spheres if sd.spheres is not None else hrt.spheres_array([]))

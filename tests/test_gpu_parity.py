@@ -565,6 +565,28 @@ def test_tail_split_bit_identical(jf):
     assert runs[0][1][0] == q
 
 
+def test_count_tests_off_bit_identical():
+    """rt_params.count_tests 0 (the library default; the test helper turns it on): the sphere program's k_trace_split
+    without its box / sphere test counters renders the same bits and queries, reports no box / sphere tests, and the
+    other kernels count as before."""
+    for sd in (scenes.config_c3(136, 80, 32), scenes.config_c5(96, 64, 16)):
+        runs = []
+        for ct in (1, 0):
+            r = scenes.make_renderer(sd)
+            r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, count_tests=ct)
+            r.draw_frames(sd.frames, 1000, 10)
+            st = r.stats()
+            runs.append((r.read_image(), st))
+        (a, sa), (b, sb) = runs
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=sd.name)
+        assert sa.queries == sb.queries and sa.box_tests > 0 and sa.sphere_tests > 0
+        if sd.mode == hrt.RT_MODE_SPHERE:
+            assert sb.box_tests == 0 and sb.sphere_tests == 0 and sb.kernel.endswith(b"false>"), sb.kernel
+        else:
+            assert (sb.box_tests, sb.sphere_tests, sb.node_tests, sb.tri_tests) == \
+                (sa.box_tests, sa.sphere_tests, sa.node_tests, sa.tri_tests)
+
+
 def test_heap_top_configs_bit_identical():
     """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 on = nodes 1..991 with 768-lane workgroups, 0 auto =
     on): the triangle program (Suzanne, the dragon with its capped walks), the mixed program with the linear and the
