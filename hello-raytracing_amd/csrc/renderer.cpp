@@ -580,13 +580,13 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         //     320+ frames loses ~2 % to one launch of every frame (C3 3 x 342 frames: 33.8 vs 34.5 Grays/s), shorter ones
         //     lose more (fewer jobs per tile spread the waves over more of the image; C3 at 82 / 164 frames 29.3 / 31.5,
         //     C4 in launches of 345 + 167 frames -13 %), so the buffer holds at most ~640 frames (C3: 8.8 GB, not 25.5),
-        //     and at most AUTO_BUDGET;
+        //     or every frame that fits AUTO_FIT if that is more, and at most AUTO_BUDGET;
         //   queue_budget_mb > 0: a cap in MiB, launches of as many frames as it holds, balanced;
         //   the fold ring (fold 0) when a launch would get fewer than min(count, 320) frames.
         // (Pipelined launches of tile-row bands x every frame, which keep every frame of a tile in one launch within a
         // bounded buffer, measured bit-identical but slower than these launches at the same budget: C3 tie, C4 -13 %,
         // C5 -19 %; profiles/r04/band/.)
-        constexpr size_t AUTO_BUDGET = 32768ull << 20;
+        constexpr size_t AUTO_BUDGET = 32768ull << 20, AUTO_FIT = 8192ull << 20;
         const size_t frame_floats = (size_t)ntiles * 64u * 3u;  // tile-padded
         const size_t frame_bytes = frame_floats * 4u;
         const uint32_t nframes_all = std::max(count, 1u);
@@ -600,9 +600,13 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             return (uint32_t)(cj <= fit ? cj : c);
         };
         if (r->params.queue_budget_mb == 0u) {
+            // the 320-frame rule, or as many frames as AUTO_FIT holds when that is more (a renderer with few rows —
+            // a rank of a multi-GPU render, C3 / 8 = 3.2 GB — draws in one launch, without the extra drains)
             const uint32_t n = std::max(1u, nframes_all / 320u);
             const size_t c = (nframes_all + n - 1u) / n, cj = (c + jf - 1u) / jf * jf;
-            budget = std::min(AUTO_BUDGET, std::min<size_t>(cj, nframes_all) * frame_bytes);
+            const size_t frames =
+                std::max(std::min<size_t>(cj, nframes_all), std::min<size_t>(AUTO_FIT / frame_bytes, nframes_all));
+            budget = std::min(AUTO_BUDGET, frames * frame_bytes);
         }
         uint32_t chunk = balanced(budget / frame_bytes), log2s = 0;
         P.ring_mode = chunk < std::min(nframes_all, 320u) ? 1u : 0u;

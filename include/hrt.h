@@ -72,11 +72,12 @@ typedef struct rt_params {
                                   grid pulling 8x8-tile x job_frames jobs, colours folded in frame
                                   order); bit-identical                       */
     uint32_t queue_budget_mb;  /* sample-queue colour memory: 0 (default) auto = the sample buffer in
-                                  floor(frames / 320) balanced launches (at least one): 320-639 frames of
-                                  colours, at most 32 GiB (C3: 3 x 342 frames, 8.5 GB); else a cap in MiB:
-                                  balanced launches of as many frames as it holds. The fold ring (bounded
-                                  memory, slower) when a launch would get fewer than min(frames, 320)
-                                  frames                                                   */
+                                  floor(frames / 320) balanced launches of whole jobs (at least one), or as
+                                  many frames per launch as 8 GiB holds if that is more, at most 32 GiB
+                                  (C3: 352 + 352 + 320 frames, 8.8 GB; a rank of an 8-way C3: one launch);
+                                  else a cap in MiB: balanced launches of as many frames as it holds. The
+                                  fold ring (bounded memory, slower) when a launch would get fewer than
+                                  min(frames, 320) frames                                 */
     uint32_t job_frames;       /* sample queue: frames per job (a job = one 8x8 tile), rounded down to a
                                   power of two (at most 1024); default 0 = per kernel: 32 with the
                                   suspendable walks, 16 for the linear sphere scans                      */

@@ -179,13 +179,13 @@ def test_sample_queue_chunks_and_tris_mode():
         assert (mb << 19) < ring <= (mb << 20) + 4 * (4 * 64 * mb + 4), st.fold_bytes
         np.testing.assert_array_equal(r.read_image().view(np.uint32), ref.read_image().view(np.uint32))
     # 320x240 = 1200 tiles, 0.92 MB of colours per frame: 320 MiB hold 364 frames (>= 320: the sample buffer)
-    # -> 700 frames in two balanced launches of whole jobs, 352 + 348; the default budget (auto: floor(700 / 320) = 2
-    # launches) the same; 1000 MiB hold all 700 frames: one launch
+    # -> 700 frames in two balanced launches of whole jobs, 352 + 348; the default budget (auto: every frame that
+    # 8 GiB holds) and 1000 MiB hold all 700 frames: one launch
     per_frame = 1200 * 64 * 12
     ref = scenes.make_renderer(sd)
     ref.set_params(schedule=hrt.RT_SCHEDULE_TILES)
     ref.draw_frames(700, 1000, 10)
-    for mb, nl, chunk in ((320, 2, 352), (None, 2, 352), (1000, 1, 700)):
+    for mb, nl, chunk in ((320, 2, 352), (None, 1, 700), (1000, 1, 700)):
         r = scenes.make_renderer(sd)
         r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **({"queue_budget_mb": mb} if mb else {}))
         r.draw_frames(700, 1000, 10)
@@ -217,6 +217,25 @@ def _queue_render(sd, frames: int, **params):
     r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **params)
     r.draw_frames(frames, 1000, 10)
     return r.read_image(), r.stats()
+
+
+def test_default_budget_launches_of_320_frames():
+    """The default colour budget on a draw whose colours exceed 8 GiB: floor(frames / 320) balanced launches of whole
+    jobs (1080p x 700 frames = 17.4 GB of colours: 352 + 348 frames, 8.8 GB), bit-identical to one launch of every
+    frame (a 32 GiB cap)."""
+    sd = scenes.golden_scene("metal_materials", 1920, 1080)
+    runs = []
+    for mb in (None, 32768):
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, **({"queue_budget_mb": mb} if mb else {}))
+        r.draw_frames(700, 1000, 10)
+        runs.append((r.read_image(), r.stats()))
+    (a, sa), (b, sb) = runs
+    per_frame = 240 * 135 * 64 * 12
+    assert sa.trace_launches == 2 and sa.launch_frames == 352 and sa.fold_bytes == 352 * per_frame, sa
+    assert sb.trace_launches == 1 and sb.launch_frames == 700, sb
+    assert sa.queries == sb.queries
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_fold_allocation_failure_shrinks_the_launches():
