@@ -563,9 +563,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // k_trace_split_tris<.., HL > 0> (heap top in LDS, 8 leaf-pair list words per lane): the mixed program's
         // sphere walk (culling BVH, begin phase) fits an 8-entry stack (a path holds at most depth pending siblings;
         // deeper trees would only fall back to the exact full scan, but keep the 16-entry kernel for them)
+        // (and heaps of at most 2^24 nodes: node_hit_so addresses node i with a 24-bit multiply-add)
         P.tri_small = 0u;
         if (r->mode != RT_MODE_SPHERE &&
-            (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u)
+            (r->mode == RT_MODE_TRIS || variant != hrt_dev::SCAN_BVH || r->bvh_host.depth <= 8u) && r->params.heap_lds != 1u &&
+            r->bvh_n <= (1u << 24))
             P.tri_small = HRT_HEAP_AUTO;
         if (variant == hrt_dev::SCAN_DEFER && r->mode == RT_MODE_MIXED && P.tri_small > 1u) P.tri_small = 1u;
         // job_frames 0 = per kernel: 32 for the suspendable walks (C3 +0.7 %, C4 +1.5 % over 16), 16 for k_trace's

@@ -99,8 +99,9 @@ typedef struct rt_params {
     uint32_t fold;             /* sample queue colour fold: 0 auto (by queue_budget_mb, above), 1 the sample
                                   buffer + k_accumulate, 2 the fold ring (bounded memory); bit-identical */
     uint32_t heap_lds;         /* triangle / mixed programs: the top of the implicit heap in LDS, 0 auto = on,
-                                  1 off (every node from L1/L2), 2 on: nodes 1..991 (768-lane workgroups;
-                                  nodes 1..255 with the deferred sphere scan); bit-identical always        */
+                                  1 off (every node from L1/L2), 2 on: nodes 1..1023 as sign-ordered nodes
+                                  (768-lane workgroups; nodes 1..255 with the deferred sphere scan; heaps of
+                                  at most 2^24 nodes); bit-identical always                               */
     uint32_t steal;            /* sample queue with the sample buffer, suspendable-walk kernels: frame-block work
                                   stealing (a wave whose job queue is drained claims single frames of other
                                   waves' jobs, so no long job trails the launch): 0 auto = on for launches of

@@ -607,8 +607,8 @@ def test_count_tests_off_bit_identical():
 
 
 def test_heap_top_configs_bit_identical():
-    """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 on = nodes 1..991 with 768-lane workgroups, 0 auto =
-    on): the triangle program (Suzanne, the dragon with its capped walks), the mixed program with the linear and the
+    """The heap's top in LDS (rt_params.heap_lds: 1 none, 2 on = nodes 1..1023, sign-ordered, with 768-lane
+    workgroups, 0 auto = on): the triangle program (Suzanne, the dragon with its capped walks), the mixed program with the linear and the
     culling-BVH sphere scans; images and ray / node / triangle counts equal across the configurations, with and
     without work stealing, and the oracle's. (The 8- and 9-level tops of round 3 were retired.)"""
     cases = [scenes.config_c4(120, 72, 5)]
