@@ -919,6 +919,30 @@ def test_tiny_heaps_leaf_pairs_vs_oracle(k):
         assert (st.queries, st.node_tests, st.tri_tests) == want, (schedule, want)
 
 
+def test_sign_ordered_fallback_vs_oracle():
+    """The heap-top kernels' reference-form fallback (rt_kernels.hip node_hit_so<.., false>): a tree with a NaN bound
+    clears so_ok, so every walk tests nodes with intersect_node's min / max on the sign-ordered layout; and an inverted
+    node (min > max on one axis, swapped by the host's packing). Images and node / triangle counts equal the oracle's,
+    which walks the unmodified node bytes."""
+    sd = scenes.config_c4(64, 40, 3)
+    sizes, nodes, tris, mats = sd.bvh
+    nodes = nodes.copy()
+    nodes["bound_min"][5, 0] = np.float32("nan")  # NaN: minNum drops it in the reference's min / max
+    mn, mx = nodes["bound_min"][9, 1].copy(), nodes["bound_max"][9, 1].copy()
+    nodes["bound_min"][9, 1], nodes["bound_max"][9, 1] = mx, mn  # inverted on y
+    sd.bvh = (sizes, nodes, tris, mats)
+    ref, q = scenes.oracle_render(sd)
+    from oracle import oracle as O
+    want = (q, O.last_counts["node_tests"], O.last_counts["tri_tests"])
+    for heap_lds in (0, 1):  # the sign-ordered layout (fallback form) and the plain node bytes
+        r = scenes.make_renderer(sd)
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, heap_lds=heap_lds)
+        r.draw_frames(sd.frames, 1000, 10)
+        assert_parity(r.read_image(), ref, f"NaN / inverted nodes, heap_lds {heap_lds}")
+        st = r.stats()
+        assert (st.queries, st.node_tests, st.tri_tests) == want, (heap_lds, want)
+
+
 @pytest.mark.parametrize("schedule", [1, 2])
 @pytest.mark.parametrize("variant", [1, 3, 4])
 def test_mixed_mode_suzanne_ground_vs_oracle(variant, schedule):
