@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Pipelined bands vs one launch: the band GPU tests, kernel-trace timelines, and interleaved bench A/B on C3/C4/C5
 # (C5 at 1024 spp) with the 8 GiB budget against 32 GiB (one launch for C3 / C4).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

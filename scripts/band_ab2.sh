@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Bands with one side stream (sequential band traces; folds beside them) vs two, at 8 GiB, against one launch;
 # then the suspend_below re-tune (scripts/sweep_r4.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

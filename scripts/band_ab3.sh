@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Bands (8 GiB) with frame-block stealing forced on (short band launches of C4 / C5 trail on a few long jobs), against
 # one launch and plain bands; C5 at its full 4096 spp.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

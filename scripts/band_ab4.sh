@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Drain-fold bands (four buffers; band i folds band i - 2 in its drain): parity tests, then 8 GiB bands against one
 # launch (32 GiB) on C3 / C4 / C5 (C4 also with stealing forced on for the band launches).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Bands (drain fold, four buffers; no auto-steal on covered bands) against the same build without bands
 # (lib/libhrt_nob.so, -DHRT_BANDS=0: frame chunks of the whole image) at the same budget; then a kernel-trace
 # timeline of C5 at 1024 spp in bands.

@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Historical: the pipelined band launches this measured were removed after these A/Bs (commit 512dacf); the
+# results are in profiles/r04/band/. The lines' config no longer carries a 'bands' field.)
 # Kernel-trace timestamps of one C4 and one C3 draw (sample buffer): with a budget below the draw's colours the
 # draw runs as pipelined bands — do consecutive band launches overlap, and how long are their drains?
 # usage: scripts/band_trace.sh [budget MiB] [tag]
