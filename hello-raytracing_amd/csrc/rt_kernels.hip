@@ -984,15 +984,33 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
     r.d = lambert ? hemi : (MODE == MODE_SPHERE ? normalize_exact(u) : normalize(u));
 }
 
+// (a, b) / sqrt(fma(b, b, a * a)) for two rng floats (each 0 or in [2^-32, 1]; the AA jitter and the disk direction
+// of make_ray): the fast correctly rounded sqrt / division sequences (rt_device.hpp, ranges as normalize_rng) unless
+// both are 0 (0 / 0: the IEEE operations give the reference's NaN); bit-identical either way. FAST false: IEEE.
+template <bool FAST>
+__device__ __forceinline__ void div_by_len_rng(float a, float b, float& qa, float& qb) {
+    const float d = __builtin_fmaf(b, b, a * a);
+    if (FAST && d >= 0x1p-100f) {  // not both 0: d in [2^-64, 2], the length in [2^-32, 1.5]
+        const RcpRN r = rcp_rn_setup(sqrt_rn_mid(d));
+        qa = div_rn_mid(a, r);
+        qb = div_rn_mid(b, r);
+    } else {
+        const float l = __builtin_sqrtf(d);
+        qa = a / l;
+        qb = b / l;
+    }
+}
+
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
 template <int MODE>
 __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
     s = (x * C->H + y) * time;
     const float r1 = rng_float(s);
     const float r2 = rng_float(s);
-    const float l = __builtin_sqrtf(__builtin_fmaf(r2, r2, r1 * r1));
-    const float px = ((float)x + 0.5f) + r1 / l;
-    const float py = ((float)y + 0.5f) + r2 / l;
+    float j1, j2;
+    div_by_len_rng<MODE == MODE_SPHERE>(r1, r2, j1, j2);
+    const float px = ((float)x + 0.5f) + j1;
+    const float py = ((float)y + 0.5f) + j2;
     const float ux = (2.0f * (px / C->wm1) - 1.0f) * C->aspect;
     const float uy = (2.0f * (py / C->hm1) - 1.0f) * -1.0f;
     float v[4];
@@ -1005,11 +1023,12 @@ __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uin
     // random_on_disk (:118-122): +x,+y quadrant unit vector times rng*radius, in world xy.
     const float q1 = rng_float(s);
     const float q2 = rng_float(s);
-    const float lq = __builtin_sqrtf(__builtin_fmaf(q2, q2, q1 * q1));
+    float e1, e2;
+    div_by_len_rng<MODE == MODE_SPHERE>(q1, q2, e1, e2);
     const float rr = rng_float(s) * C->blur;
     float o4[4];
-    o4[0] = C->eye[0] + (q1 / lq) * rr;
-    o4[1] = C->eye[1] + (q2 / lq) * rr;
+    o4[0] = C->eye[0] + e1 * rr;
+    o4[1] = C->eye[1] + e2 * rr;
     o4[2] = C->eye[2] + 0.0f * rr;
     o4[3] = C->eye[3] + 1.0f;
     Ray r;
