@@ -234,9 +234,21 @@ __device__ __forceinline__ float sqrt_rn_mid(float x) {
 struct RcpRN {
     float l, r;
 };
-__device__ __forceinline__ RcpRN rcp_rn_setup(float l) {
+// The refined reciprocal: v_rcp_f32 (<= 1 ulp) and one Newton step whose residual 1 - l r0 is exact. It is
+// itself RN(1 / l) for |l| in [2^-60, 2^60]: for every significand and every r0 within 1 ulp of 1 / l the step
+// lands on the correctly rounded value except r0 = 2^k under an all-ones significand, where r0 + r0 (1 - l r0)
+// is a tie that rounds back to r0 (tests/test_rcp_exact.py enumerates both); the GPU self-check
+// (k_check_exact_math) runs every significand through v_rcp_f32 itself.
+__device__ __forceinline__ float rcp_rn_mid(float l) {
     const float r0 = __builtin_amdgcn_rcpf(l);
-    return RcpRN{l, __builtin_fmaf(__builtin_fmaf(-l, r0, 1.0f), r0, r0)};
+    return __builtin_fmaf(__builtin_fmaf(-l, r0, 1.0f), r0, r0);
+}
+__device__ __forceinline__ RcpRN rcp_rn_setup(float l) { return RcpRN{l, rcp_rn_mid(l)}; }
+// 1 / l, bit-identical to the IEEE division: the refined reciprocal where |l| lies in [2^-60, 2^60], else `/`.
+__device__ __forceinline__ float rcp_exact(float l) {
+    const float al = __builtin_fabsf(l);
+    if (al >= 0x1p-60f && al <= 0x1p60f) return rcp_rn_mid(l);
+    return 1.0f / l;
 }
 __device__ __forceinline__ float div_rn_mid(float x, const RcpRN& d) {
     float q = x * d.r;

@@ -225,7 +225,9 @@ int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 
 /* Self-check of the kernels' range-restricted correctly rounded sqrt / division sequences against the IEEE
  * operations on n random cases each (diagnostics): mismatches[0] normalize of rng
- * vectors and normalize_exact of signed vectors, [1] division on [2^-60, 2^60], [2] sqrt on [2^-100, 2^100].
+ * vectors and normalize_exact of signed vectors, [1] division on [2^-60, 2^60] and the reciprocal of every
+ * significand (case i's operand is fixed by i: n = 2^30 covers each under 128 signs / exponents in [2^-60, 2^60]),
+ * [2] sqrt on [2^-100, 2^100].
  * All three must be 0. */
 int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]);
 
