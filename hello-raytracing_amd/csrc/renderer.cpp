@@ -472,6 +472,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         cd.aspect = (float)r->width / (float)r->height;
         cd.wm1 = (float)r->width - 1.0f;
         cd.hm1 = (float)r->height - 1.0f;
+        // for the fast exact divisions of make_ray's px / wm1, py / hm1 (div_rn_mid's operand range)
+        const auto inv_in_range = [](float l) { return l >= 0x1p-60f && l <= 0x1p60f ? 1.0f / l : 0.0f; };
+        cd.inv_wm1 = inv_in_range(cd.wm1);
+        cd.inv_hm1 = inv_in_range(cd.hm1);
         cd.H = r->height;
     }
     P.W = r->width;

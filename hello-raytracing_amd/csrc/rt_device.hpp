@@ -96,6 +96,7 @@ struct CamDev {
     float eye[4], dir[4], up[4], right[4];
     float focal, blur, k;         // k = tan(fov / 2), host libm tanf
     float aspect, wm1, hm1;       // f32(W)/f32(H), f32(W) - 1, f32(H) - 1 (host, same IEEE ops)
+    float inv_wm1, inv_hm1;       // 1 / wm1, 1 / hm1 correctly rounded (host), 0 outside [2^-60, 2^60]
     uint32_t H, pad;
 };
 

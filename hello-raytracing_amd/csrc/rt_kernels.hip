@@ -1014,6 +1014,15 @@ __device__ __forceinline__ void div_by_len_rng(float a, float b, float& qa, floa
     }
 }
 
+// x / l for make_ray's px / wm1 and py / hm1: FAST (sphere program), div_rn_mid with the host's correctly rounded
+// 1 / l where l (inv != 0) and x lie in its range [2^-60, 2^60] (x = pixel + 0.5 + jitter >= 0.5; a NaN jitter takes
+// the division); else the IEEE division. Bit-identical either way.
+template <bool FAST>
+__device__ __forceinline__ float div_cam(float x, float l, float inv) {
+    if (FAST && inv != 0.0f && x >= 0x1p-60f && x <= 0x1p60f) return div_rn_mid(x, RcpRN{l, inv});
+    return x / l;
+}
+
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
 template <int MODE>
 __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
@@ -1024,15 +1033,32 @@ __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uin
     div_by_len_rng<MODE == MODE_SPHERE>(r1, r2, j1, j2);
     const float px = ((float)x + 0.5f) + j1;
     const float py = ((float)y + 0.5f) + j2;
-    const float ux = (2.0f * (px / C->wm1) - 1.0f) * C->aspect;
-    const float uy = (2.0f * (py / C->hm1) - 1.0f) * -1.0f;
+    const float ux = (2.0f * div_cam<MODE == MODE_SPHERE>(px, C->wm1, C->inv_wm1) - 1.0f) * C->aspect;
+    const float uy = (2.0f * div_cam<MODE == MODE_SPHERE>(py, C->hm1, C->inv_hm1) - 1.0f) * -1.0f;
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) v[i] = ((C->right[i] * ux) * C->k + (C->up[i] * uy) * C->k) + C->dir[i];
-    const float lv = __builtin_sqrtf(__builtin_fmaf(v[3], v[3], __builtin_fmaf(v[2], v[2], __builtin_fmaf(v[1], v[1], v[0] * v[0]))));
+    const float dv = __builtin_fmaf(v[3], v[3], __builtin_fmaf(v[2], v[2], __builtin_fmaf(v[1], v[1], v[0] * v[0])));
+    float vn[4];
+    // sphere program: v / |v| by the fast sequences where |v0..2| lie in [2^-40, 2^40] and |v3| <= 2^40 (dv, the
+    // length and the quotients inside their ranges, as normalize_exact); v[3] / |v| is unused there (f4[3])
+    const float vlo = fmin_ieee(fmin_ieee(__builtin_fabsf(v[0]), __builtin_fabsf(v[1])), __builtin_fabsf(v[2]));
+    const float vhi = fmax_ieee(fmax_ieee(__builtin_fabsf(v[0]), __builtin_fabsf(v[1])),
+                                fmax_ieee(__builtin_fabsf(v[2]), __builtin_fabsf(v[3])));
+    if (MODE == MODE_SPHERE && vlo >= 0x1p-40f && vhi <= 0x1p40f) {
+        const float lv = sqrt_rn_mid(dv);
+        const RcpRN rl = rcp_rn_setup(lv);
+#pragma unroll
+        for (int i = 0; i < 3; i++) vn[i] = div_rn_mid(v[i], rl);
+        vn[3] = v[3] / lv;
+    } else {
+        const float lv = __builtin_sqrtf(dv);
+#pragma unroll
+        for (int i = 0; i < 4; i++) vn[i] = v[i] / lv;
+    }
     float f4[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) f4[i] = C->eye[i] + (v[i] / lv) * C->focal;
+    for (int i = 0; i < 4; i++) f4[i] = C->eye[i] + vn[i] * C->focal;
     // random_on_disk (:118-122): +x,+y quadrant unit vector times rng*radius, in world xy.
     const float q1 = rng_float(s);
     const float q2 = rng_float(s);
