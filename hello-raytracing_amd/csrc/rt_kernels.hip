@@ -376,6 +376,69 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
     // overflow and finished are kept as integers (VGPRs): an i1 lane mask carried through the nested
     // divergent loops of k_trace_split was observed to keep stale overflow bits (sticky full scans)
     uint32_t overflow = 0u, finished = 0u;
+#ifndef HRT_BTEST
+#define HRT_BTEST 1
+#endif
+    if constexpr (SELECT && NOOVF && SO && HRT_BTEST) {
+        // k_trace_split's walk with the descent as a bottom-tested loop (one exit: a miss, or a leaf reached), the
+        // same visits in the same order as the loop below
+        while (true) {
+            if (!(node & BVH_LEAF_BIT)) {
+                bool any;
+                do {
+#ifdef HRT_STAMPS
+                    if constexpr (SUSPEND) {
+                        tally.lbox++;
+                        if (first_active_lane()) tally.wbox++;
+                    }
+#endif
+                    float tl, tr;
+                    const uint4 c0 = hn[2 * node], c1 = hn[2 * node + 1];
+                    const bool hl = box_hit_so(c0.x, c0.y, c0.z, shx, shy, shz, S, bt, tl);
+                    const bool hr = box_hit_so(c1.x, c1.y, c1.z, shx, shy, shz, S, bt, tr);
+                    if constexpr (COUNT) tally.boxes += 2;
+                    const bool lfirst = hl && (!hr || tl <= tr);
+                    const uint32_t near = lfirst ? c0.w : c1.w, far = lfirst ? c1.w : c0.w;
+                    const bool both = hl && hr;
+                    any = hl || hr;
+                    if (both) stack[sp * LS] = far;
+                    sp += both ? 1 : 0;
+                    node = any ? near : node;
+                } while (any && !(node & BVH_LEAF_BIT));
+            }
+            if (node & BVH_LEAF_BIT) {
+#ifdef HRT_STAMPS
+                if constexpr (SUSPEND) {
+                    tally.lleaf++;
+                    if (first_active_lane()) tally.wleaf++;
+                }
+#endif
+                const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+                    const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((first + j) * 16u), 0, 0);
+                    const float t = exact_t_geo<true>(float4{v.x, v.y, v.z, v.w}, r, a4, a2);
+                    if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
+                        const __amdgpu_buffer_rsrc_t rsl =
+                            __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+                        const int slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)((first + j) * 4u), 0, 0);
+                        if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
+                    }
+                }
+                if constexpr (COUNT) tally.spheres += cnt;
+            }
+            if (sp == 0) {
+                finished = 1u;
+                break;
+            }
+            node = stack[(--sp) * LS];
+            if constexpr (SUSPEND) {
+                if ((uint32_t)__popcll(__ballot(1)) < below) break;
+            }
+        }
+    } else
     while (true) {
         if (!(node & BVH_LEAF_BIT)) {
 #ifdef HRT_STAMPS
