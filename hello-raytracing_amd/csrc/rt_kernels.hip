@@ -379,9 +379,11 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #ifndef HRT_BTEST
 #define HRT_BTEST 1
 #endif
-    if constexpr (SELECT && NOOVF && SO && HRT_BTEST) {
-        // k_trace_split's walk with the descent as a bottom-tested loop (one exit: a miss, or a leaf reached), the
-        // same visits in the same order as the loop below
+    if constexpr (NOOVF && SO && HRT_BTEST) {
+        // The sign-ordered walks without overflow (k_trace_split with LDS nodes, the HL3 mixed kernels) with the
+        // descent as a bottom-tested loop: one exit (a miss, or a leaf reached) and the node / stack depth updated
+        // in place, where the top-tested form below kept two loop-header copies and more exec-mask bookkeeping
+        // per box step (C3 +3.2 %). Same visits in the same order (the child order is the three-way form's).
         while (true) {
             if (!(node & BVH_LEAF_BIT)) {
                 bool any;
@@ -415,15 +417,26 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #endif
                 const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
                 for (uint32_t j = 0; j < cnt; j++) {
-                    typedef float f4v __attribute__((ext_vector_type(4)));
-                    const __amdgpu_buffer_rsrc_t rs =
-                        __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
-                    const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((first + j) * 16u), 0, 0);
-                    const float t = exact_t_geo<true>(float4{v.x, v.y, v.z, v.w}, r, a4, a2);
+                    float4 g;
+                    if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        const __amdgpu_buffer_rsrc_t rs =
+                            __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+                        const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((first + j) * 16u), 0, 0);
+                        g = float4{v.x, v.y, v.z, v.w};
+                    } else {
+                        g = P.bvh_sph[first + j];
+                    }
+                    const float t = exact_t_geo<SELECT>(g, r, a4, a2);
                     if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
-                        const __amdgpu_buffer_rsrc_t rsl =
-                            __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
-                        const int slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)((first + j) * 4u), 0, 0);
+                        int slot;
+                        if constexpr (SELECT) {
+                            const __amdgpu_buffer_rsrc_t rsl =
+                                __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+                            slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)((first + j) * 4u), 0, 0);
+                        } else {
+                            slot = P.bvh_slot[first + j];
+                        }
                         if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                     }
                 }
