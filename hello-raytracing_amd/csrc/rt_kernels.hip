@@ -858,6 +858,7 @@ __device__ __forceinline__ bool heap_run(const KParams& P, const Ray& r, HeapWal
     while (true) {
         while (walking != 0u && __ballot(nc == CAP) == 0ull) {
             step++;
+            asm volatile("" : "+v"(step));  // the branches below add to this value, not to the last trip's
             bool hit;
             if constexpr (HT > 0) hit = node_hit_so<HT, SO, FULL>(i, r.o, inv, tb, ox, oy, oz);
             else hit = node_hit(P, i, r.o, inv);
