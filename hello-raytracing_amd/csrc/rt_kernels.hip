@@ -379,6 +379,9 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #ifndef HRT_BTEST
 #define HRT_BTEST 1
 #endif
+#ifndef HRT_LEAFIV
+#define HRT_LEAFIV 1
+#endif
     if constexpr (NOOVF && SO && HRT_BTEST) {
         // The sign-ordered walks without overflow (k_trace_split with LDS nodes, the HL3 mixed kernels) with the
         // descent as a bottom-tested loop: one exit (a miss, or a leaf reached) and the node / stack depth updated
@@ -416,6 +419,33 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 }
 #endif
                 const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+#if HRT_LEAFIV
+                // one induction variable: the sphere's byte offset (slot word at o / 4, BVH position o / 16)
+                for (uint32_t o = first * 16u, oe = (first + cnt) * 16u; o != oe; o += 16u) {
+                    float4 g;
+                    if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        const __amdgpu_buffer_rsrc_t rs =
+                            __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+                        const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
+                        g = float4{v.x, v.y, v.z, v.w};
+                    } else {
+                        g = P.bvh_sph[o >> 4];
+                    }
+                    const float t = exact_t_geo<SELECT>(g, r, a4, a2);
+                    if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
+                        int slot;
+                        if constexpr (SELECT) {
+                            const __amdgpu_buffer_rsrc_t rsl =
+                                __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+                            slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)(o >> 2), 0, 0);
+                        } else {
+                            slot = P.bvh_slot[o >> 4];
+                        }
+                        if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(o >> 4); }
+                    }
+                }
+#else
                 for (uint32_t j = 0; j < cnt; j++) {
                     float4 g;
                     if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
@@ -440,6 +470,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                         if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(first + j); }
                     }
                 }
+#endif
                 if constexpr (COUNT) tally.spheres += cnt;
             }
             if (sp == 0) {
