@@ -303,15 +303,18 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
                         4.0001e-23f * __builtin_amdgcn_rsqf(a);
     const float pad = 2.02f * delta;
     Q.S.inv = mk(robust_inv(r.d.x), robust_inv(r.d.y), robust_inv(r.d.z));
-    Q.S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
-    Q.S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+    if constexpr (SO) {
+        // near / far: the pad signed like 1/d (x - (-p) = x + p exactly: the same two constants, swapped where 1/d < 0)
+        const f3 ps = mk(__builtin_copysignf(pad, Q.S.inv.x), __builtin_copysignf(pad, Q.S.inv.y),
+                         __builtin_copysignf(pad, Q.S.inv.z));
+        Q.S.lo = mk(-op.x - ps.x, -op.y - ps.y, -op.z - ps.z);
+        Q.S.hi = mk(-op.x + ps.x, -op.y + ps.y, -op.z + ps.z);
+    } else {
+        Q.S.lo = mk(-op.x - pad, -op.y - pad, -op.z - pad);
+        Q.S.hi = mk(-op.x + pad, -op.y + pad, -op.z + pad);
+    }
     Q.S.lo = Q.S.lo * Q.S.inv;
     Q.S.hi = Q.S.hi * Q.S.inv;
-    if constexpr (SO) {
-        const f3 lo = Q.S.lo, hi = Q.S.hi;
-        Q.S.lo = mk(Q.S.inv.x < 0.0f ? hi.x : lo.x, Q.S.inv.y < 0.0f ? hi.y : lo.y, Q.S.inv.z < 0.0f ? hi.z : lo.z);
-        Q.S.hi = mk(Q.S.inv.x < 0.0f ? lo.x : hi.x, Q.S.inv.y < 0.0f ? lo.y : hi.y, Q.S.inv.z < 0.0f ? lo.z : hi.z);
-    }
     Q.node = P.bvh_root;
     return true;
 }
