@@ -779,6 +779,9 @@ __device__ __forceinline__ void tri_record(const KParams& P, const Ray& r, const
     h.front = dot(h.n, r.d) > 0.0f;
 }
 
+#ifndef HRT_TRI_NESTED
+#define HRT_TRI_NESTED 1
+#endif
 // The reference's per-leaf update: accept t in [1e-4, best). The walks only track (best, bj); the hit
 // record is built once for the winner (closest_hit), which keeps fewer registers live during the walk.
 template <bool TBUF = false>
@@ -796,7 +799,25 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
     } else {
         tr = P.tris[j];
     }
+#if HRT_TRI_NESTED
+    // tri_t's tests as nested branches (no -1 sentinel carried to a merge: its moves and select per triangle)
+    const f3 e1 = mk(tr.e1.x, tr.e1.y, tr.e1.z);
+    const f3 e2 = mk(tr.e2.x, tr.e2.y, tr.e2.z);
+    const f3 hh = cross(r.d, e2);
+    const float det = dot(e1, hh);
+    if (__builtin_fabsf(det) < 1e-4f) return;
+    float inv_det = rcp_rn_mid(det);
+    if (__builtin_expect(!(__builtin_fabsf(det) <= 0x1p60f), 0)) inv_det = 1.0f / det;
+    const f3 s = r.o - mk(tr.a.x, tr.a.y, tr.a.z);
+    const float u = inv_det * dot(s, hh);
+    if (u < 0.0f || u > 1.0f) return;
+    const f3 q = cross(s, e1);
+    const float v = inv_det * dot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return;
+    const float t = inv_det * dot(e2, q);
+#else
     const float t = tri_t(r, tr);
+#endif
     if (t >= 1e-4f && t < best) {
         best = t;
         bj = (int)j;
