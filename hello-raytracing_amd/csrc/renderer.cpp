@@ -898,8 +898,10 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.job_frames = 0;  // per kernel (rt_draw_frames)
     // measured: C3 (sphere) 0 -> 21.2, 8 -> 23.4, 16 -> 23.8, 24 -> 23.7, 32 -> 22.7 Grays/s (first split
     //           kernel); with the frame-block refill and 16-frame jobs 16 -> 25.2, 24 -> 25.9, 32 -> 25.2;
-    //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92
-    r->params.suspend_below = mode == RT_MODE_SPHERE ? 24u : 32u;
+    //           C4 (mixed) 0 -> 7.02, 8 -> 7.74, 16 -> 8.00, 24 -> 8.15, 32 -> 8.22, 48 -> 7.92; round 4 (final
+    //           kernels, profiles/r04/so/sweep_sb_mixed.txt): C4 24 = 32 (13.22), C5 16/20/24/28/32 -> 10.26/10.27/
+    //           10.30/10.28/10.24: the mixed program takes 24 too, the triangle program keeps 32
+    r->params.suspend_below = mode == RT_MODE_TRIS ? 32u : 24u;
     bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&r->ev_start) == hipSuccess && hipEventCreate(&r->ev_stop) == hipSuccess;
     if (!ok) {

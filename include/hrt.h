@@ -89,8 +89,8 @@ typedef struct rt_params {
                                   program; reference heap walk of the triangle / mixed programs) once
                                   fewer than this many of its 64 lanes are still walking, so finished
                                   lanes shade and start their next query instead of idling (0 = no wave
-                                  leaves a walk before all of its lanes finish); default 24 (sphere) / 32
-                                  (others); not used by tri_bvh = 1 or the linear sphere scans.
+                                  leaves a walk before all of its lanes finish); default 24 (sphere and
+                                  mixed) / 32 (triangle); not used by tri_bvh = 1 or the linear sphere scans.
                                   Bit-identical either way                      */
     uint32_t row_block;        /* rows per block of the row partition (default 1; 0 reads as 1): the renderer
                                   owns rows row0 + k*row_step*row_block + j, j < row_block, in that order.

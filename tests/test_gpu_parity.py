@@ -1058,5 +1058,6 @@ def test_bad_arguments_fail_loudly():
         with pytest.raises(hrt.RtError):  # removed variants, unknown schedule / tree, empty partition,
             r.set_params(**bad)           # a suspend threshold above the wave width
     assert hrt.Renderer(8, 8, hrt.RT_MODE_SPHERE).params.suspend_below == 24  # per-program defaults
+    assert hrt.Renderer(8, 8, hrt.RT_MODE_MIXED).params.suspend_below == 24
     assert r.params.suspend_below == 32
     assert r.params.job_frames == 0  # per kernel: 32 with the suspendable walks, 16 for the linear scans
