@@ -1156,17 +1156,19 @@ __device__ __forceinline__ float div_cam(float x, float l, float inv) {
 }
 
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
-template <int MODE>
+// FASTRNG: the jitter / disk / px, py divisions by the fast exact sequences (the sphere program everywhere; the other
+// programs' split kernels, whose frame-block refill has the registers for them — k_render<2, 4, false> spilled)
+template <int MODE, bool FASTRNG = (MODE == MODE_SPHERE)>
 __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
     s = (x * C->H + y) * time;
     const float r1 = rng_float(s);
     const float r2 = rng_float(s);
     float j1, j2;
-    div_by_len_rng<MODE == MODE_SPHERE>(r1, r2, j1, j2);
+    div_by_len_rng<FASTRNG>(r1, r2, j1, j2);
     const float px = ((float)x + 0.5f) + j1;
     const float py = ((float)y + 0.5f) + j2;
-    const float ux = (2.0f * div_cam<MODE == MODE_SPHERE>(px, C->wm1, C->inv_wm1) - 1.0f) * C->aspect;
-    const float uy = (2.0f * div_cam<MODE == MODE_SPHERE>(py, C->hm1, C->inv_hm1) - 1.0f) * -1.0f;
+    const float ux = (2.0f * div_cam<FASTRNG>(px, C->wm1, C->inv_wm1) - 1.0f) * C->aspect;
+    const float uy = (2.0f * div_cam<FASTRNG>(py, C->hm1, C->inv_hm1) - 1.0f) * -1.0f;
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) v[i] = ((C->right[i] * ux) * C->k + (C->up[i] * uy) * C->k) + C->dir[i];
@@ -1195,7 +1197,7 @@ __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uin
     const float q1 = rng_float(s);
     const float q2 = rng_float(s);
     float e1, e2;
-    div_by_len_rng<MODE == MODE_SPHERE>(q1, q2, e1, e2);
+    div_by_len_rng<FASTRNG>(q1, q2, e1, e2);
     const float rr = rng_float(s) * C->blur;
     float o4[4];
     o4[0] = C->eye[0] + e1 * rr;
@@ -2248,7 +2250,7 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             uint32_t ps = 0;
             const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
             const uint32_t time = K->time0 + (B.job_f0 + B.blk_f) * K->dtime;
-            if (pok) pr = primary_ray<MODE>(&kargs()->cam, x, y, time, ps);
+            if (pok) pr = primary_ray<MODE, true>(&kargs()->cam, x, y, time, ps);
             float* const e = blk + BW * threadIdx.x;
             e[0] = pr.o.x;
             e[1] = pr.o.y;
