@@ -147,24 +147,33 @@ def launcher_selftest(args) -> int:
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    # 37 rows: with 8-row blocks rank 4 of 5+ would own none; the rows carry their index and the column
-    H, W = 37, 5
     block = args.row_block
-    rows = rank_rows(rank, world, H, block)
-    part = torch.zeros((max_rows(world, H, block), W, 3), dtype=torch.float32)
-    part[: len(rows)] = (torch.from_numpy(rows.astype("float32"))[:, None, None] * 16.0
-                         + torch.arange(W, dtype=torch.float32)[None, :, None])
-    t0 = time.perf_counter()
-    full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0, block=block)
-    gather_s = time.perf_counter() - t0
-    local = {"rows": len(rows), "elapsed_s": 0.0, "trace_ms": 0.0, "gather_ms": gather_s * 1e3, "queries": 0,
-             "checksum": image_checksum(part, rows, W)}
-    report = rank_reports(local, world, dist if world > 1 else None, "cpu")
+
+    def leg(H, W):
+        rows = rank_rows(rank, world, H, block)
+        part = torch.zeros((max_rows(world, H, block), W, 3), dtype=torch.float32)
+        part[: len(rows)] = (torch.from_numpy(rows.astype("float32"))[:, None, None] * 16.0
+                             + torch.arange(W, dtype=torch.float32)[None, :, None])
+        t0 = time.perf_counter()
+        full = gather_image(part, H, dist if world > 1 else None, rank, world, dst=0, block=block)
+        gather_s = time.perf_counter() - t0
+        # (no renderer, no GPU: the device fields stay -1 and the device check reports null)
+        local = {"rows": len(rows), "elapsed_s": 0.0, "trace_ms": 0.0, "gather_ms": gather_s * 1e3, "queries": 0,
+                 "checksum": image_checksum(part, rows, W)}
+        report = rank_reports(local, world, dist if world > 1 else None, "cpu")
+        ok = rank != 0 or bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32) * 16.0))
+        return report, (image_checksum(full, range(H), W) if rank == 0 else 0), ok
+
+    # 37 rows: with 8-row blocks rank 4 of 5+ would own none; the rows carry their index and the column. Then the
+    # second leg of a multi-rank bench (C5, run after the headline config) on another shape.
+    report, full_sum, ok = leg(37, 5)
+    report5, full_sum5, ok5 = leg(53, 7)
     if rank == 0:
-        ok = bool(torch.equal(full[:, 0, 0], torch.arange(H, dtype=torch.float32) * 16.0))
         out = {"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}", "row_block": block,
                "verify_gather_bitwise": ok}
-        out.update(multi_rank_fields(report, image_checksum(full, range(H), W), 1))
+        out.update(multi_rank_fields(report, full_sum, 1))
+        out["c5"] = {"config": {"id": "c5", "width": 7, "height": 53}, "steps": 1, "verify_gather_bitwise": ok5,
+                     **multi_rank_fields(report5, full_sum5, 1)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -172,14 +181,26 @@ def launcher_selftest(args) -> int:
     return 0
 
 
+REPORT_KEYS = ("rows", "elapsed_s", "trace_ms", "gather_ms", "queries", "device", "pci", "torch_device", "torch_pci")
+
+
+def pci_code(pci) -> int:
+    """(domain, bus, device) as one integer (-1: no GPU)."""
+    return -1 if pci is None else (int(pci[0]) << 16) | (int(pci[1]) << 8) | int(pci[2])
+
+
+def pci_str(code: int):
+    return None if code < 0 else f"{code >> 16:04x}:{(code >> 8) & 0xFF:02x}:{code & 0xFF:02x}"
+
+
 def rank_reports(local: dict, world: int, dist, device) -> list:
     """Every rank's own figures (rows owned, timed-region wall time, trace kernel time, gather time, rays, image
-    checksum), collected on every rank by one all_gather after the timed region (the 8-GPU run is the
-    driver's alone, so its line must say what each rank did)."""
+    checksum, and the GPU it drew on: the renderer's device (rt_get_device) next to torch's current device, each as
+    ordinal and PCI location), collected on every rank by one all_gather after the timed region (the
+    8-GPU run is the driver's alone, so its line must say what each rank did, and where)."""
     import torch
 
-    keys = ("rows", "elapsed_s", "trace_ms", "gather_ms", "queries")
-    t = torch.tensor([float(local[k]) for k in keys], dtype=torch.float64, device=device)
+    t = torch.tensor([float(local.get(k, -1)) for k in REPORT_KEYS], dtype=torch.float64, device=device)
     # (the checksum as a signed 64-bit word)
     c = torch.tensor([((int(local["checksum"]) + 2**63) % 2**64) - 2**63], dtype=torch.int64, device=device)
     if dist is None:
@@ -192,25 +213,50 @@ def rank_reports(local: dict, world: int, dist, device) -> list:
     out = []
     for k in range(world):
         v = ts[k].cpu().tolist()
-        d = {"rank": k, **{key: v[i] for i, key in enumerate(keys)}, "checksum": int(cs[k].cpu().item())}
-        d["rows"], d["queries"] = int(d["rows"]), int(d["queries"])
+        d = {"rank": k, **{key: v[i] for i, key in enumerate(REPORT_KEYS)}, "checksum": int(cs[k].cpu().item())}
+        for key in ("rows", "queries", "device", "pci", "torch_device", "torch_pci"):
+            d[key] = int(d[key])
         out.append(d)
     return out
 
 
-def multi_rank_fields(report: list, full_checksum: int, steps: int) -> dict:
-    """The JSON line's per-rank block: per-rank elapsed / trace / gather times and rows, the gather's own time, and
-    the destination rank's check that the gathered image's position-dependent checksum equals the sum of the ranks'
-    local ones (hrt.parallel.image_checksum; mod 2^64)."""
+def device_check(report: list, distinct: bool):
+    """(ok, message): every rank's renderer draws on its torch device (same ordinal and PCI location) and, with one
+    GPU per rank (nccl), no two ranks share a GPU. None when the ranks have no GPU (the CPU launcher self-test)."""
+    if any(d["device"] < 0 or d["torch_device"] < 0 for d in report):
+        return None, None
+    bad = [d["rank"] for d in report if (d["device"], d["pci"]) != (d["torch_device"], d["torch_pci"])]
+    if bad:
+        return False, (f"ranks {bad}: the renderer's GPU differs from torch's current device (two HIP runtimes, or "
+                       f"set_device not seen by the renderer)")
+    if distinct:
+        seen = {}
+        for d in report:
+            seen.setdefault(d["pci"], []).append(d["rank"])
+        shared = {pci_str(k): v for k, v in seen.items() if len(v) > 1}
+        if shared:
+            return False, f"ranks share a GPU: {shared}"
+    return True, None
+
+
+def multi_rank_fields(report: list, full_checksum: int, steps: int, distinct_gpus: bool = True) -> dict:
+    """The JSON line's per-rank block: per-rank elapsed / trace / gather times, rows and GPU (renderer and torch), the
+    gather's own time, the destination rank's check that the gathered image's position-dependent checksum equals the
+    sum of the ranks' local ones (hrt.parallel.image_checksum; mod 2^64), and the device check (device_check)."""
     ranks = [{"rank": d["rank"], "rows": d["rows"], "elapsed_s": round(d["elapsed_s"], 4),
               "trace_ms_per_step": round(d["trace_ms"] / steps, 3), "gather_ms_per_step": round(d["gather_ms"] / steps, 3),
-              "rays_per_step": round(d["queries"] / steps)} for d in report]
+              "rays_per_step": round(d["queries"] / steps),
+              "device": d["device"], "pci": pci_str(d["pci"]), "torch_device": d["torch_device"],
+              "torch_pci": pci_str(d["torch_pci"])} for d in report]
     total = sum(d["checksum"] for d in report)
+    ok, msg = device_check(report, distinct_gpus)
     return {
         "ranks": ranks,
         "gather_ms_per_step": round(max(d["gather_ms"] for d in report) / steps, 3),
         "slowest_rank": max(report, key=lambda d: d["elapsed_s"])["rank"],
         "gather_checksum_ok": (total - int(full_checksum)) % 2**64 == 0,
+        "device_check_ok": ok,
+        "device_error": msg,
     }
 
 
@@ -239,6 +285,16 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
 
 
 MODE_NAMES = {0: "sphere", 1: "tris", 2: "mixed"}
+# the frame protocol of every timed step (the reference's golden tests: time 1000 + 10 i, rendering_tests.rs:14-28)
+TIME0, DTIME = 1000, 10
+
+
+def timed_knobs(frames_per_launch: int = 1024, variant: int = 0, schedule: int = 0, tri_bvh: int = 0, **extra) -> dict:
+    """rt_params of the timed draws (the library's defaults unless a flag overrides them): count_tests 0, so the sphere
+    program's k_trace_split runs uncounted (its box / sphere counts come from a counting warmup draw, bit-identical).
+    tests/test_gpu_timed.py renders the timed configurations through this same function."""
+    return dict(frames_per_launch=frames_per_launch, variant=variant, schedule=schedule, tri_bvh=tri_bvh,
+                count_tests=0, **extra)
 
 
 def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_rays: float) -> dict:
@@ -261,7 +317,7 @@ def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_r
 
         def share_step():
             rk.reset_frame_count()
-            rk.draw_frames(sd.frames, 1000, 10)
+            rk.draw_frames(sd.frames, TIME0, DTIME)
             rk.copy_image_to_device(buf.data_ptr(), buf.numel())
             return rk.stats()
 
@@ -299,6 +355,105 @@ def emulate_split(sd, knobs: dict, n: int, args, full_img, full_s: float, full_r
         "bitwise_equal_full_image": same,
         "per_rank": shares,
     }
+
+
+def run_leg(sd, knobs: dict, args, dist, rank: int, world: int, dev, steps: int, warmup: int, tag: str = "") -> dict:
+    """One timed leg of the bench on this rank: the renderer for this rank's rows (8-row blocks dealt round-robin),
+    `warmup` counting steps, then `steps` timed steps bracketed by a barrier + synchronize on both sides. A step =
+    reset, draw every frame (TIME0 + f * DTIME), copy the image into the rank's band, gather the bands on rank 0."""
+    import torch
+
+    import scenes
+    from hrt.parallel import gather_image, image_checksum, max_rows, owned_rows, rank_params
+
+    r = scenes.make_renderer(sd)
+    r.set_params(**rank_params(rank, world, args.row_block), **knobs)
+    local_rows = r.local_rows
+    part = torch.zeros((max_rows(world, sd.height, args.row_block), sd.width, 3), dtype=torch.float32, device=dev)
+    gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
+    full = torch.empty((sd.height, sd.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    gather_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    gather_ms = [0.0]
+
+    def step():
+        r.reset_frame_count()
+        r.draw_frames(sd.frames, TIME0, DTIME)
+        r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
+        st = r.stats()
+        gather_ev[0].record()
+        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=args.row_block)
+        gather_ev[1].record()
+        if world > 1:
+            # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
+            # renderer's own stream, which does not order against it: finish the gather first
+            torch.cuda.current_stream().synchronize()
+        gather_ev[1].synchronize()
+        gather_ms[0] += gather_ev[0].elapsed_time(gather_ev[1])
+        return st
+
+    log(f"{tag + ' ' if tag else ''}rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, "
+        f"{len(sd.spheres) if sd.spheres is not None else 0} spheres, {local_rows} rows, warmup {warmup}")
+    counted = None  # (box tests, sphere tests) of one step, from a counting draw
+
+    def counting_step():
+        r.set_params(count_tests=1)
+        st = step()
+        r.set_params(count_tests=0)
+        return st.box_tests, st.sphere_tests
+
+    for i in range(warmup):
+        t = time.perf_counter()
+        counted = counting_step()
+        torch.cuda.synchronize()
+        log(f"{tag} warmup {i}: {time.perf_counter() - t:.2f} s")
+
+    barrier()
+    gather_ms[0] = 0.0
+    t0 = time.perf_counter()
+    L = {"queries": 0, "kernel_ms": 0.0, "launches": 0, "box_tests": 0, "sphere_tests": 0, "node_tests": 0,
+         "tri_tests": 0, "variant": 0, "schedule": 0, "suspend": 0, "trace_ms": 0.0, "trace_launches": 0,
+         "st_last": None}
+    uncounted = False
+    for i in range(steps):
+        st = step()
+        L["st_last"] = st
+        for k in ("queries", "kernel_ms", "launches", "box_tests", "sphere_tests", "node_tests", "tri_tests",
+                  "trace_ms", "trace_launches"):
+            L[k] += getattr(st, k)
+        uncounted = st.box_tests == 0 and st.sphere_tests == 0
+        L["variant"], L["schedule"], L["suspend"] = st.variant, st.schedule, st.suspend_below
+        log(f"{tag} step {i}: {st.queries / 1e9:.3f} G rays, kernels {st.kernel_ms:.1f} ms (trace {st.trace_ms:.1f}), "
+            f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
+    barrier()
+    L["elapsed"] = time.perf_counter() - t0
+    if steps and uncounted:  # the timed kernels did not count: the per-step counts of a counting draw
+        if counted is None:  # (no warmup: one more draw after the timed region, rank-local, no collective)
+            r.set_params(count_tests=1)
+            r.reset_frame_count()
+            r.draw_frames(sd.frames, TIME0, DTIME)
+            st_c = r.stats()
+            r.set_params(count_tests=0)
+            counted = (st_c.box_tests, st_c.sphere_tests)
+        L["box_tests"], L["sphere_tests"] = counted[0] * steps, counted[1] * steps
+    # this rank's report: rows, times, rays, its band's position-dependent checksum, and the GPU it drew on — the
+    # renderer's (rt_get_device) next to torch's current device
+    ordinal, pci = r.device()
+    tdev = torch.cuda.current_device()
+    tp = torch.cuda.get_device_properties(tdev)
+    p = rank_params(rank, world, args.row_block)
+    L["local"] = {"rows": local_rows, "elapsed_s": L["elapsed"], "trace_ms": L["trace_ms"], "gather_ms": gather_ms[0],
+                  "queries": L["queries"], "device": ordinal, "pci": pci_code(pci), "torch_device": tdev,
+                  "torch_pci": pci_code((tp.pci_domain_id, tp.pci_bus_id, tp.pci_device_id)),
+                  "checksum": image_checksum(part, owned_rows(p["row0"], p["row_step"], sd.height, args.row_block),
+                                             sd.width)}
+    L.update(renderer=r, full=full, local_rows=local_rows)
+    return L
 
 
 def main() -> int:
@@ -344,6 +499,11 @@ def main() -> int:
     ap.add_argument("--emulate-ranks", type=int, default=None,
                     help="single-GPU proxy of the N-rank split: render every rank's share here in turn after the "
                          "timed region (default 8 on a one-rank run, 0 = off)")
+    ap.add_argument("--c5-leg", type=int, default=None,
+                    help="after the timed config, time a short C5 leg (BASELINE's 8-GPU config): default on for "
+                         "multi-rank runs, 1 forces it on one rank, 0 off")
+    ap.add_argument("--c5-steps", type=int, default=3)
+    ap.add_argument("--c5-warmup", type=int, default=1)
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU-only rehearsal of the multi-rank path (self-launch, gloo, row-tile gather): no GPU")
     args = ap.parse_args()
@@ -357,12 +517,11 @@ def main() -> int:
     if args.launcher_selftest:
         return launcher_selftest(args)
 
-    import numpy as np
     import torch
 
     import hrt  # noqa: F401  (loads lib/libhrt.so)
     import scenes
-    from hrt.parallel import gather_image, image_checksum, max_rows, owned_rows, rank_params
+    from hrt.parallel import image_checksum
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -390,7 +549,6 @@ def main() -> int:
         sd.height = args.height or sd.height
         sd.frames = args.frames or sd.frames
     nslots = len(sd.spheres)
-    r = scenes.make_renderer(sd)
     extra = {} if args.suspend_below is None else {"suspend_below": args.suspend_below}
     if args.job_frames is not None:
         extra["job_frames"] = args.job_frames
@@ -407,107 +565,17 @@ def main() -> int:
     # the timed draws run the default kernels (count_tests 0: the sphere program's k_trace_split does not count its box
     # and sphere tests); the warmup draws count them (count_tests 1) for the per-ray figures of the line, the same
     # every step (bit-identical draws)
-    knobs = dict(frames_per_launch=args.frames_per_launch, variant=args.variant, schedule=args.schedule,
-                 tri_bvh=args.tri_bvh, count_tests=0, **extra)
-    r.set_params(**rank_params(rank, world, args.row_block), **knobs)
-    local_rows = r.local_rows
-    part = torch.zeros((max_rows(world, sd.height, args.row_block), sd.width, 3), dtype=torch.float32, device=dev)
-    gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
-    full = torch.empty((sd.height, sd.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    gather_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    gather_ms = [0.0]
-
-    def step():
-        r.reset_frame_count()
-        r.draw_frames(sd.frames, 1000, 10)
-        r.copy_image_to_device(part.data_ptr(), local_rows * sd.width * 3)  # syncs the renderer stream
-        st = r.stats()
-        gather_ev[0].record()
-        gather_image(part, sd.height, dist, rank, world, dst=0, gathered=gathered, out=full, block=args.row_block)
-        gather_ev[1].record()
-        if world > 1:
-            # the gather reads `part` on the collective's stream; the next step's copy into `part` runs on the
-            # renderer's own stream, which does not order against it: finish the gather first
-            torch.cuda.current_stream().synchronize()
-        gather_ev[1].synchronize()
-        gather_ms[0] += gather_ev[0].elapsed_time(gather_ev[1])
-        return st
-
-    log(f"rank {rank}/{world}: {sd.name} {sd.width}x{sd.height} x{sd.frames} frames, {nslots} spheres, "
-        f"{local_rows} rows, warmup {args.warmup}")
-    counted = None  # (box tests, sphere tests) of one step, from a counting draw
-
-    def counting_step():
-        r.set_params(count_tests=1)
-        st = step()
-        r.set_params(count_tests=0)
-        return st.box_tests, st.sphere_tests
-
-    for i in range(args.warmup):
-        t = time.perf_counter()
-        counted = counting_step()
-        torch.cuda.synchronize()
-        log(f"warmup {i}: {time.perf_counter() - t:.2f} s")
-
-    barrier()
-    gather_ms[0] = 0.0
-    t0 = time.perf_counter()
-    queries = 0
-    kernel_ms = 0.0
-    launches = 0
-    box_tests = 0
-    sphere_tests = 0
-    node_tests = 0
-    tri_tests = 0
-    variant = 0
-    schedule = 0
-    suspend = 0
-    trace_ms = 0.0
-    trace_launches = 0
-    st_last = None
-    uncounted = False
-    for i in range(args.steps):
-        st = step()
-        st_last = st
-        queries += st.queries
-        kernel_ms += st.kernel_ms
-        launches += st.launches
-        box_tests += st.box_tests
-        sphere_tests += st.sphere_tests
-        uncounted = st.box_tests == 0 and st.sphere_tests == 0
-        node_tests += st.node_tests
-        tri_tests += st.tri_tests
-        variant = st.variant
-        schedule = st.schedule
-        suspend = st.suspend_below
-        trace_ms += st.trace_ms
-        trace_launches += st.trace_launches
-        log(f"step {i}: {st.queries / 1e9:.3f} G rays, kernels {st.kernel_ms:.1f} ms (trace {st.trace_ms:.1f}), "
-            f"{st.sphere_tests / max(st.queries, 1):.1f} sphere + {st.box_tests / max(st.queries, 1):.1f} box tests/ray")
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if args.steps and uncounted:  # the timed kernels did not count: the per-step counts of a counting draw
-        if counted is None:  # (no warmup: one more draw after the timed region, rank-local, no collective)
-            r.set_params(count_tests=1)
-            r.reset_frame_count()
-            r.draw_frames(sd.frames, 1000, 10)
-            st_c = r.stats()
-            r.set_params(count_tests=0)
-            counted = (st_c.box_tests, st_c.sphere_tests)
-        box_tests, sphere_tests = counted[0] * args.steps, counted[1] * args.steps
+    knobs = timed_knobs(args.frames_per_launch, args.variant, args.schedule, args.tri_bvh, **extra)
+    L = run_leg(sd, knobs, args, dist, rank, world, dev, args.steps, args.warmup)
+    full, local_rows, elapsed, queries = L["full"], L["local_rows"], L["elapsed"], L["queries"]
+    st_last, schedule, suspend, variant = L["st_last"], L["schedule"], L["suspend"], L["variant"]
     emulated = None
     n_emul = args.emulate_ranks if args.emulate_ranks is not None else (8 if world == 1 else 0)
     if world == 1 and n_emul > 1:
         emulated = emulate_split(sd, knobs, n_emul, args, full, elapsed / args.steps, queries / args.steps)
 
-    stats_t = torch.tensor([elapsed, float(queries), trace_ms, float(trace_launches), float(box_tests),
-                            float(sphere_tests), float(node_tests), float(tri_tests), kernel_ms],
+    stats_t = torch.tensor([elapsed, float(queries), L["trace_ms"], float(L["trace_launches"]), float(L["box_tests"]),
+                            float(L["sphere_tests"]), float(L["node_tests"]), float(L["tri_tests"]), L["kernel_ms"]],
                            dtype=torch.float64,
                            device=dev if args.backend == "nccl" else "cpu")
     if dist is not None:
@@ -518,16 +586,24 @@ def main() -> int:
         all_t = stats_t.cpu().numpy()[None]
     t_max = float(all_t[:, 0].max())
     total_q = float(all_t[:, 1].sum())
-    # per-rank figures and the gather's checksum check (multi-rank runs)
+    # per-rank figures, the gather's checksum check and the device check (multi-rank runs)
     report = None
+    coll_dev = dev if args.backend == "nccl" else "cpu"
     if world > 1:
-        local = {"rows": local_rows, "elapsed_s": elapsed, "trace_ms": trace_ms, "gather_ms": gather_ms[0],
-                 "queries": queries,
-                 "checksum": image_checksum(part, owned_rows(*[rank_params(rank, world, args.row_block)[k]
-                                                               for k in ("row0", "row_step")], sd.height,
-                                                             args.row_block), sd.width)}
-        report = rank_reports(local, world, dist, dev if args.backend == "nccl" else "cpu")
+        report = rank_reports(L["local"], world, dist, coll_dev)
+    # BASELINE.json's 8-GPU config is C5 (4K x 4096 spp, row tiles + RCCL gather): after the headline leg a multi-rank
+    # run times a short C5 leg too (1 warmup + 3 steps; ~1.2 s per step on 8 ranks), same partition, same report
+    c5 = None
+    c5_on = args.c5_leg if args.c5_leg is not None else (world > 1 and args.config != "c5")
+    if c5_on:
+        sd5 = scenes.CONFIGS["c5"]()
+        L5 = run_leg(sd5, timed_knobs(args.frames_per_launch, 0, 0, 0), args, dist, rank, world, dev, args.c5_steps,
+                     args.c5_warmup, tag="c5")
+        rep5 = rank_reports(L5["local"], world, dist, coll_dev)
+        c5 = {"L": L5, "report": rep5, "sd": sd5}
+        del L5["renderer"]
 
+    device_error = None
     if rank == 0:
         value = total_q / t_max / 1e6
         # roofline of the ray-tracing kernel (k_trace under the sample queue, k_render under tiles) on
@@ -630,8 +706,35 @@ def main() -> int:
                 "pmc": pmc_view(pmc),
             },
         }
+        # one GPU per rank under RCCL: no two ranks may share one (a gloo rehearsal on one GPU shares it by design)
+        distinct = args.backend == "nccl"
+        device_error = None
         if report is not None:
-            out.update(multi_rank_fields(report, image_checksum(full, range(sd.height), sd.width), args.steps))
+            out.update(multi_rank_fields(report, image_checksum(full, range(sd.height), sd.width), args.steps, distinct))
+            device_error = out["device_error"]
+        if c5 is not None:
+            L5, rep5, sd5 = c5["L"], c5["report"], c5["sd"]
+            t5 = max(d["elapsed_s"] for d in rep5)
+            q5 = sum(d["queries"] for d in rep5)
+            st5 = L5["st_last"]
+            blk = {
+                "metric": f"Mrays/sec, {sd5.name} {sd5.width}x{sd5.height}x{sd5.frames}spp x {sd5.bounces}-bounce",
+                "value": round(q5 / t5 / 1e6, 2),
+                "unit": "Mrays/s",
+                "steps": args.c5_steps,
+                "warmup": args.c5_warmup,
+                "ms_per_step": round(t5 / max(args.c5_steps, 1) * 1e3, 2),
+                "config": {"workload": sd5.name, "id": "c5", "width": sd5.width, "height": sd5.height, "spp": sd5.frames,
+                           "bounces": sd5.bounces, "spheres": len(sd5.spheres), "parallelism": f"rows{world}",
+                           "row_block": args.row_block, "rays_per_step": round(q5 / max(args.c5_steps, 1)),
+                           "kernel": st5.kernel.decode() if st5 is not None else "",
+                           "launch_frames": int(st5.launch_frames) if st5 is not None else 0,
+                           "trace_launches_per_step": int(st5.trace_launches) if st5 is not None else 0},
+            }
+            blk.update(multi_rank_fields(rep5, image_checksum(L5["full"], range(sd5.height), sd5.width),
+                                         max(args.c5_steps, 1), distinct))
+            device_error = device_error or blk["device_error"]
+            out["c5"] = blk
         if emulated is not None:
             out["emulated_split"] = emulated
         if not args.no_cpu_baseline and world == 1:
@@ -645,16 +748,18 @@ def main() -> int:
             # rehearsal check: the gathered image equals one renderer drawing every row (bitwise)
             ref_r = scenes.make_renderer(sd)
             ref_r.set_params(**knobs)
-            ref_r.draw_frames(sd.frames, 1000, 10)
+            ref_r.draw_frames(sd.frames, TIME0, DTIME)
             ref_img = torch.from_numpy(ref_r.read_image())
             same = torch.equal(full.cpu().view(torch.int32), ref_img.view(torch.int32))
             out["verify_gather_bitwise"] = bool(same)
             log(f"verify: gathered image {'==' if same else '!='} single-renderer image")
         print(json.dumps(out), flush=True)
+        if device_error:
+            log(f"DEVICE CHECK FAILED: {device_error}")
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return 3 if (rank == 0 and device_error) else 0
 
 
 if __name__ == "__main__":

@@ -94,7 +94,7 @@ struct Tree {
     std::vector<Triangle> triangles;
     std::vector<Material> materials;
     void add_mesh(const Mesh& mesh);  // tree.rs:74-90
-    void build(unsigned threads = 0);  // tree.rs:36-72; threads 0 = HRT_HOST_THREADS or min(16, cores)
+    void build(unsigned threads = 0);  // tree.rs:36-72; threads 0 = min(16, cores)
 };
 
 // render_ppm.rs:38-57 (pixel formatting part).

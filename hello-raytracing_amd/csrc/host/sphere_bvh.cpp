@@ -47,16 +47,16 @@ struct Builder {
     std::vector<Prim> prims;
     SphereBvh* out;
     uint32_t max_depth = 0;
-    // leaf policy (HRT_BVH_MAX_LEAF / HRT_BVH_LEAF_DEPTH / HRT_BVH_TRAVERSAL_COST override, for tuning)
+    // leaf policy (fixed: the library reads no environment variable; tuned values below)
     uint32_t max_leaf = BVH_MAX_LEAF;
     uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
     double traversal_cost = 0.5;
-    // binned SAH over all three axes (HRT_BVH_ALL_AXES=0: the widest axis, 16 bins, as first built). C3,
+    // binned SAH over all three axes (all_axes false: the widest axis, 16 bins, as first built). C3,
     // Grays/s by bin count: 8 25.9, 16 26.8, 24 26.9, 32 27.7, 48 26.8, 64 28.0 (box / sphere tests per ray
     // 16.0 / 4.5 at 64, 16.8 / 5.4 first); an exact sweep SAH gave 26.9: tree shape matters more than
     // SAH accuracy here, and 64 bins measured best
     bool all_axes = true;
-    int bins = 64;  // HRT_BVH_BINS (2..64) with all_axes
+    int bins = 64;  // 2..64 with all_axes
 
     uint32_t leaf_word(size_t first, size_t count) {
         uint32_t f = (uint32_t)out->slot.size();

@@ -1024,15 +1024,22 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
         md[k] = hrt_dev::MatDev{M[k].albedo.x, M[k].albedo.y, M[k].albedo.z, M[k].params.x, M[k].kind,
                                 dc.inv_param, dc.r0sq_front, dc.r0sq_back};
     }
-    bool so_ok = true;
-    const std::vector<float> so = pack_nodes_so((const float*)nodes32, n, so_ok);
+    // The sign-ordered copy (36 B per node) only where a kernel reads it: the heap-top kernels run for heaps of at
+    // most 2^24 nodes (launch_frames, tri_small); a larger tree would pay up to ~2.4 GB of host and device memory
+    // for nothing
+    const bool want_so = n <= (1u << 24);
+    bool so_ok = false;
+    std::vector<float> so;
+    if (want_so) so = pack_nodes_so((const float*)nodes32, n, so_ok);
+    else r->nodes_so.release();
     int rc = ensure(r->nodes, 2 * (size_t)std::max<uint32_t>(n, 1));
-    if (!rc) rc = ensure(r->nodes_so, so.size());
+    if (!rc && want_so) rc = ensure(r->nodes_so, so.size());
     if (!rc) rc = ensure(r->tris, std::max<uint32_t>(m, 1));
     if (!rc) rc = ensure(r->mats, std::max<uint32_t>(n_mats, 1));
     if (rc) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(r->nodes.ptr, nodes32, (size_t)n * 32u, hipMemcpyHostToDevice, r->stream));
-    HIP_TRY(hipMemcpyAsync(r->nodes_so.ptr, so.data(), so.size() * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    if (want_so)
+        HIP_TRY(hipMemcpyAsync(r->nodes_so.ptr, so.data(), so.size() * sizeof(float), hipMemcpyHostToDevice, r->stream));
     if (m) HIP_TRY(hipMemcpyAsync(r->tris.ptr, td.data(), (size_t)m * sizeof(td[0]), hipMemcpyHostToDevice, r->stream));
     if (n_mats)
         HIP_TRY(hipMemcpyAsync(r->mats.ptr, md.data(), (size_t)n_mats * sizeof(md[0]), hipMemcpyHostToDevice, r->stream));
@@ -1198,6 +1205,17 @@ int rt_get_wave_trace(rt_renderer* r, uint64_t* out, size_t n_words) {
     if (ds.rc) return ds.rc;
     if (n_words > r->wave_trace_words) return fail(RT_ERR_ARG, "rt_get_wave_trace: more words than recorded");
     if (n_words) HIP_TRY(hipMemcpy(out, r->wave_trace.ptr, n_words * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_get_device(const rt_renderer* r, int32_t* ordinal, int32_t pci[3]) {
+    if (!r || !ordinal || !pci) return fail(RT_ERR_ARG, "rt_get_device: null");
+    int v[3] = {0, 0, 0};
+    HIP_TRY(hipDeviceGetAttribute(&v[0], hipDeviceAttributePciDomainId, r->device));
+    HIP_TRY(hipDeviceGetAttribute(&v[1], hipDeviceAttributePciBusId, r->device));
+    HIP_TRY(hipDeviceGetAttribute(&v[2], hipDeviceAttributePciDeviceId, r->device));
+    *ordinal = r->device;
+    for (int k = 0; k < 3; k++) pci[k] = v[k];
     return RT_OK;
 }
 

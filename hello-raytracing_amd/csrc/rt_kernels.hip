@@ -2206,8 +2206,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
 // compiles spill-free there): when the wave's block (one frame
 // of its job's 8x8 tile) is used up, every lane computes its own pixel's primary ray for the next frame at
-// once into the wave's slice of `blk` (o, d and, SEED, the RNG state after the primary ray: 7 floats per lane; a ragged
-// edge tile's missing pixels get d = 0, which no primary ray has), and lanes that need a sample read theirs. Without
+// once into the wave's slice of `blk` (o, d and, SEED, the RNG state after the primary ray: 7 floats per lane; the
+// block's in-image pixels as a 64-bit mask in the wave's two `okw` words — a ragged edge tile's missing pixels take no
+// sample; d = 0 is no marker: with focal_length 0 and blur 0 every primary ray of the triangle / mixed programs has
+// d = (g / |g|).xyz = 0, and the reference traces it), and lanes that need a sample read theirs. Without
 // SEED (6 floats per lane) a taken sample's RNG state is recomputed from its pixel: it starts at (x * H + y) * time
 // (primary_ray) = the row's (x0 * H + y) * time + (x - x0) * H * time, per-row words in `rows` (9 per wave), then
 // five PCG steps. (Two float4 per lane before round 4: the bytes saved hold the whole heap top.)
@@ -2217,7 +2219,7 @@ struct BlockState {
 
 template <int MODE, bool STEAL, bool SEED>
 __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
-                                                 uint32_t* rows, bool& drained,
+                                                 uint32_t* rows, uint32_t* okw, bool& drained,
                                                  uint32_t lane, unsigned long long below, bool& have,
                                                  uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
                                                  uint32_t& bounce, uint32_t& pix, uint32_t& fl) {
@@ -2251,6 +2253,14 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
             const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
             const uint32_t time = K->time0 + (B.job_f0 + B.blk_f) * K->dtime;
             if (pok) pr = primary_ray<MODE, true>(&kargs()->cam, x, y, time, ps);
+            {
+                const unsigned long long okm = __ballot(pok != 0u);
+                uint32_t* const ow = okw + 2u * (threadIdx.x >> 6);
+                if (lane == 0u) {
+                    ow[0] = (uint32_t)okm;
+                    ow[1] = (uint32_t)(okm >> 32);
+                }
+            }
             float* const e = blk + BW * threadIdx.x;
             e[0] = pr.o.x;
             e[1] = pr.o.y;
@@ -2275,9 +2285,10 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
         const float* const e = blk + BW * ((threadIdx.x & ~63u) + src);
         const float ox = e[0], oy = e[1], oz = e[2], dx = e[3], dy = e[4], dz = e[5];
         bool took = false;
+        const uint32_t okb = (okw[2u * (threadIdx.x >> 6) + (src >> 5)] >> (src & 31u)) & 1u;
         if (need && rank < avail) {
             need = false;
-            if (dx != 0.0f || dy != 0.0f || dz != 0.0f) {  // (a pixel outside the image: d = 0)
+            if (okb) {  // (a pixel outside the image: no sample)
                 ray.o = mk(ox, oy, oz);
                 ray.d = mk(dx, dy, dz);
                 if constexpr (SEED) {
@@ -2608,6 +2619,7 @@ k_trace_split_tris(const KParams P) {
     constexpr bool SEED = !(HL == 3 && SCAN == SCAN_BVH);
     __shared__ float blk[(SEED ? 7 : 6) * WGT];
     __shared__ uint32_t blk_rows[SEED ? 1 : 9 * (WGT / 64u)];
+    __shared__ uint32_t blk_ok[2 * (WGT / 64u)];  // per wave: the block's in-image pixels (64-bit mask)
     BlockState B;
     __shared__ uint32_t wjobs[(WGT / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
@@ -2623,8 +2635,8 @@ k_trace_split_tris(const KParams P) {
     HeapWalk W;
     HRT_PHASE_DECL;
     while (true) {
-        refill_block_lds<MODE, STEAL, SEED>(P, B, J, blk, blk_rows, drained, lane, below, have, qs, ray, att, sky_t, s, bounce, pix,
-                                      fl);
+        refill_block_lds<MODE, STEAL, SEED>(P, B, J, blk, blk_rows, blk_ok, drained, lane, below, have, qs, ray, att, sky_t, s,
+                                            bounce, pix, fl);
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
@@ -2787,10 +2799,11 @@ __global__ __launch_bounds__(256) void k_check_exact_math(unsigned long long n, 
         if ((mx & 0xFFu) == 0u) x = 0.0f;
         if (__float_as_uint(x / l) != __float_as_uint(div_rn_mid(x, rcp_rn_setup(l)))) bad[1]++;
         // rcp_rn_mid vs 1 / l by enumeration: case i takes significand i mod 2^23 under sign / exponent pair
-        // i >> 23 (exponents spread over [-60, 59]), so n = 2^30 runs every significand under 128 of them
+        // (i >> 23) mod 242 — both signs of every binade 2^-60 .. 2^60 (biased exponents 67 .. 187) — so n = 242 x 2^23
+        // runs every significand of the range the kernels use it on (no scaling assumption left)
         {
-            const uint32_t se = (uint32_t)(i >> 23) & 0x7Fu;
-            const uint32_t e = 67u + ((se >> 1) * 119u) / 63u;
+            const uint32_t se = (uint32_t)((i >> 23) % 242u);
+            const uint32_t e = 67u + (se >> 1);
             const float r = __uint_as_float(((se & 1u) << 31) | (e << 23) | ((uint32_t)i & 0x7FFFFFu));
             if (__float_as_uint(1.0f / r) != __float_as_uint(rcp_rn_mid(r))) bad[1]++;
         }

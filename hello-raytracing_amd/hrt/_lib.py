@@ -7,6 +7,7 @@ there is no CPU fallback anywhere in this package.
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
 import os
 from pathlib import Path
 
@@ -106,6 +107,7 @@ SIGNATURES = {
     "rt_diagnostic_build": (C.c_int, []),
     "rt_check_exact_math": (C.c_int, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "rt_get_wave_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
+    "rt_get_device": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_last_error": (C.c_char_p, []),
     "rt_device_count": (C.c_int, []),
     "rt_build_info": (C.c_char_p, []),
@@ -144,8 +146,47 @@ class RtError(RuntimeError):
         self.code = code
 
 
+def _torch_hip_runtime() -> Path | None:
+    """torch's own HIP runtime (torch/lib/libamdhip64.so), located without importing torch."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return None
+    p = Path(spec.origin).resolve().parent / "lib" / "libamdhip64.so"
+    return p if p.exists() else None
+
+
+def hip_runtimes() -> set:
+    """Real paths of the HIP runtime libraries (libamdhip64*) mapped into this process (/proc/self/maps)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and "libamdhip64" in parts[5]:
+                    out.add(os.path.realpath(parts[5]))
+    except OSError:  # pragma: no cover (no procfs: nothing to check)
+        pass
+    return out
+
+
+def check_single_hip_runtime() -> None:
+    """Raise if two HIP runtimes are mapped: a renderer then binds to a device of the runtime libhrt.so resolved while
+    torch.cuda.set_device steers the other one, so every rank of a multi-GPU run would silently draw on GPU 0
+    (VERDICT r4). lib() makes the order of imports irrelevant by preloading torch's runtime; this catches anything
+    else (an LD_PRELOAD, a library loaded by hand)."""
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise RuntimeError(f"two HIP runtimes are mapped into this process: {sorted(rts)}; libhrt.so must share "
+                           "torch's (import hrt through this module, which preloads it)")
+
+
 def lib() -> C.CDLL:
-    """Load libhrt.so once. Raises if it was not built (no fallback)."""
+    """Load libhrt.so once. Raises if it was not built (no fallback).
+
+    The HIP runtime: libhrt.so needs libamdhip64.so.7 (RUNPATH /opt/rocm); torch ships its own copy with the same
+    SONAME. Loaded first, torch's copy satisfies libhrt.so too; loaded after libhrt.so, torch would map a second
+    runtime (two device states: torch.cuda.set_device would not reach the renderer). So torch's copy, when torch is
+    installed, is preloaded here (RTLD_GLOBAL; loading it does not initialise the GPU) before libhrt.so."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
@@ -153,7 +194,11 @@ def lib() -> C.CDLL:
                 f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
                 "(or __graft_entry__.build()); the renderer has no Python/CPU fallback"
             )
+        trt = _torch_hip_runtime()
+        if trt is not None:
+            C.CDLL(os.fspath(trt), mode=C.RTLD_GLOBAL)
         L = C.CDLL(os.fspath(LIB_PATH))
+        check_single_hip_runtime()
         for name, (res, args) in {**SIGNATURES, **TESTING_SIGNATURES}.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -269,7 +269,9 @@ class Renderer:
 
     def __init__(self, width: int, height: int, mode: int):
         h = C.c_void_p()
-        check(lib().rt_create(width, height, mode, C.byref(h)), "Renderer::new")
+        L = lib()
+        _lib.check_single_hip_runtime()  # (torch may have been imported since libhrt.so was loaded)
+        check(L.rt_create(width, height, mode, C.byref(h)), "Renderer::new")
         self._h = h
         self.mode = mode
         self.width = width
@@ -284,6 +286,13 @@ class Renderer:
 
     def set_frame_count(self, n: int) -> None:
         check(lib().rt_set_frame_count(self._h, n), "set_frame_count")
+
+    def device(self) -> tuple:
+        """(HIP ordinal, (PCI domain, bus, device)) of the GPU this renderer draws on (rt_get_device)."""
+        o = C.c_int32()
+        pci = (C.c_int32 * 3)()
+        check(lib().rt_get_device(self._h, C.byref(o), pci), "rt_get_device")
+        return o.value, tuple(pci)
 
     @property
     def frame_count(self) -> int:

@@ -204,8 +204,9 @@ int rt_synchronize(rt_renderer *r);
 int rt_get_stats(const rt_renderer *r, rt_stats *out);
 /* Frees the sample queue's colour-fold memory (the sample buffer or the fold ring, rt_stats.fold_bytes)
  * after the pending draws; the next queue draw allocates it again. For a renderer kept alive between
- * renders beside other work: one C3 render holds 7.6 GB under the default budget (no reference
- * counterpart: wgpu frees nothing either, but the reference has no per-sample buffer). */
+ * renders beside other work: one C3 render holds 8.8 GB under the default budget (352 frames x 24.9 MB;
+ * rt_stats.fold_bytes has the figure of the last draw) (no reference counterpart: wgpu frees nothing
+ * either, but the reference has no per-sample buffer). */
 int rt_release_scratch(rt_renderer *r);
 
 /* Test-only entry points (fault injection) are declared in hrt_testing.h, not here: they are not part of
@@ -226,10 +227,16 @@ int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 /* Self-check of the kernels' range-restricted correctly rounded sqrt / division sequences against the IEEE
  * operations on n random cases each (diagnostics): mismatches[0] normalize of rng
  * vectors and normalize_exact of signed vectors, [1] division on [2^-60, 2^60] and the reciprocal of every
- * significand (case i's operand is fixed by i: n = 2^30 covers each under 128 signs / exponents in [2^-60, 2^60]),
- * [2] sqrt on [2^-100, 2^100].
+ * significand (case i's operand is fixed by i: n = 242 x 2^23 covers each under both signs of every binade
+ * 2^-60 .. 2^60), [2] sqrt on [2^-100, 2^100].
  * All three must be 0. */
 int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]);
+
+/* The GPU a renderer draws on (no reference counterpart; the multi-GPU bench checks every rank's renderer against
+ * its torch device): the HIP device ordinal that was current at rt_create, and that device's PCI location
+ * {domain, bus, device}. A process must load ONE HIP runtime for the ordinal to mean what the caller's runtime
+ * means (hrt/_lib.py loads the one torch uses). */
+int rt_get_device(const rt_renderer *r, int32_t *ordinal, int32_t pci[3]);
 
 /* Thread-local message for the last failing call. */
 const char *rt_last_error(void);

@@ -391,15 +391,20 @@ uint64_t oracle_render(const o_params *p, const void *camera80, const void *sphe
     sc.mode = p->mode; sc.bounces = p->bounces; sc.step_cap = p->step_cap;
     sc.eps = p->mode == MODE_SPHERE ? 1e-6f : 1e-4f;
     uint64_t total = 0, tnodes = 0, ttris = 0, tcapped = 0;
+    /* work items: (row, 64-column chunk) pairs, so a render of a few long rows (the full-frame-count checks of the
+       timed configurations: 1-3 rows x 1024-4096 frames) still spreads over every thread; pixels are independent */
+    const uint32_t XC = 64u, nxc = (p->nx + XC - 1u) / XC;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, tnodes, ttris, tcapped)
 #endif
-    for (int64_t k = 0; k < (int64_t)p->nrows; k++) {
+    for (int64_t item = 0; item < (int64_t)p->nrows * nxc; item++) {
+        const int64_t k = item / nxc;
+        const uint32_t xa = p->x0 + (uint32_t)(item % nxc) * XC, xb = xa + XC < p->x0 + p->nx ? xa + XC : p->x0 + p->nx;
         const uint32_t rb = p->row_block > 1 ? p->row_block : 1;
         uint32_t y = p->row0 + ((uint32_t)k / rb) * p->row_step * rb + (uint32_t)k % rb;
         uint64_t q[4] = {0, 0, 0, 0};
-        for (uint32_t x = p->x0; x < p->x0 + p->nx; x++) {
+        for (uint32_t x = xa; x < xb; x++) {
             float *px = image + ((size_t)k * p->nx + (x - p->x0)) * 3;
             float r = px[0], g = px[1], b = px[2];
             for (uint32_t f = 0; f < p->frames; f++) {

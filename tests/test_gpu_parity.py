@@ -1027,12 +1027,13 @@ def test_rendering_performance():
 
 def test_range_restricted_exact_math_matches_ieee():
     """The kernels' short correctly rounded sequences (hemisphere normalize, division by a shared refined
-    reciprocal, sqrt without scaling; rt_device.hpp) equal the IEEE operations bit for bit on 2^30 random
-    cases each in their stated ranges."""
+    reciprocal, sqrt without scaling; rt_device.hpp) equal the IEEE operations bit for bit on 2^30+ random
+    cases each in their stated ranges; the refined reciprocal on every significand under both signs of every binade
+    2^-60 .. 2^60 (242 x 2^23 cases: the enumeration is the case index, the same for every seed)."""
     import ctypes as C
     out = (C.c_uint64 * 3)()
-    for seed in (1, 0x9E3779B9):
-        hrt._lib.check(hrt.lib().rt_check_exact_math(1 << 30, seed, out), "rt_check_exact_math")
+    for seed, n in ((1, 242 << 23), (0x9E3779B9, 1 << 30)):
+        hrt._lib.check(hrt.lib().rt_check_exact_math(n, seed, out), "rt_check_exact_math")
         assert list(out) == [0, 0, 0], list(out)
 
 

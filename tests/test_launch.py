@@ -44,16 +44,48 @@ def test_bench_self_launches_ranks_and_gathers(world):
     assert {k: res[k] for k in ("launcher_selftest", "n_gpus", "parallelism", "row_block", "verify_gather_bitwise")} == \
         {"launcher_selftest": True, "n_gpus": world, "parallelism": f"rows{world}", "row_block": 8,
          "verify_gather_bitwise": True}
-    assert res["gather_checksum_ok"] is True
-    ranks = res["ranks"]
-    assert [d["rank"] for d in ranks] == list(range(world))
-    assert [d["rows"] for d in ranks] == [len(rank_rows(k, world, 37, 8)) for k in range(world)]
-    assert sum(d["rows"] for d in ranks) == 37
-    for d in ranks:
-        assert set(d) == {"rank", "rows", "elapsed_s", "trace_ms_per_step", "gather_ms_per_step", "rays_per_step"}
-        assert d["gather_ms_per_step"] >= 0.0
-    assert res["gather_ms_per_step"] == max(d["gather_ms_per_step"] for d in ranks)
-    assert 0 <= res["slowest_rank"] < world
+    fields = {"rank", "rows", "elapsed_s", "trace_ms_per_step", "gather_ms_per_step", "rays_per_step", "device", "pci",
+              "torch_device", "torch_pci"}
+    # the headline leg (37 rows) and the C5 leg of a multi-rank run (53 rows here)
+    for blk, H in ((res, 37), (res["c5"], 53)):
+        assert blk["gather_checksum_ok"] is True
+        ranks = blk["ranks"]
+        assert [d["rank"] for d in ranks] == list(range(world))
+        assert [d["rows"] for d in ranks] == [len(rank_rows(k, world, H, 8)) for k in range(world)]
+        assert sum(d["rows"] for d in ranks) == H
+        for d in ranks:
+            assert set(d) == fields
+            assert d["gather_ms_per_step"] >= 0.0
+            # no GPU in the self-test: the renderer / torch device fields are present and empty
+            assert (d["device"], d["pci"], d["torch_device"], d["torch_pci"]) == (-1, None, -1, None)
+        assert blk["gather_ms_per_step"] == max(d["gather_ms_per_step"] for d in ranks)
+        assert 0 <= blk["slowest_rank"] < world
+        assert blk["device_check_ok"] is None and blk["device_error"] is None
+    assert res["c5"]["config"]["id"] == "c5" and res["c5"]["verify_gather_bitwise"] is True
+
+
+def _report(world, devices, pcis, tdevices=None, tpcis=None):
+    return [{"rank": k, "rows": 1, "elapsed_s": 0.0, "trace_ms": 0.0, "gather_ms": 0.0, "queries": 0, "checksum": 0,
+             "device": devices[k], "pci": pcis[k], "torch_device": (tdevices or devices)[k],
+             "torch_pci": (tpcis or pcis)[k]} for k in range(world)]
+
+
+def test_device_check_fails_the_line_on_a_wrong_or_shared_gpu():
+    """bench.device_check: each rank's renderer must draw on torch's current device, and under RCCL
+    no two ranks may share a GPU. The cases a one-GPU box cannot produce, on synthetic reports."""
+    import bench
+
+    pci = [bench.pci_code((0, 0x05 + 0x10 * k, 0)) for k in range(4)]
+    assert bench.device_check(_report(4, [0, 1, 2, 3], pci), True) == (True, None)
+    # every renderer on GPU 0 while torch moved each rank to its own GPU (two HIP runtimes)
+    ok, msg = bench.device_check(_report(4, [0, 0, 0, 0], [pci[0]] * 4, [0, 1, 2, 3], pci), True)
+    assert ok is False and "ranks [1, 2, 3]" in msg
+    # two ranks on one GPU (both consistent with torch): fails under RCCL, allowed in a gloo rehearsal
+    shared = [pci[0], pci[1], pci[1], pci[3]]
+    ok, msg = bench.device_check(_report(4, [0, 1, 1, 3], shared), True)
+    assert ok is False and "0000:15:00" in msg and "[1, 2]" in msg
+    assert bench.device_check(_report(4, [0, 1, 1, 3], shared), False) == (True, None)
+    assert bench.pci_str(bench.pci_code((1, 0xC3, 2))) == "0001:c3:02"
 
 
 def test_image_checksum_catches_misplaced_rows():
