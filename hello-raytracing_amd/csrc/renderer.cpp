@@ -516,7 +516,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.counter = r->counter.ptr;
 #ifdef HRT_STAMPS
     {
-        const size_t words = 4ull * ((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u;
+        // k_render's waves, or the persistent kernels' (at most steal_cap = 32 per CU)
+        const size_t words = 4ull * std::max<size_t>((size_t)((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u,
+                                                     32ull * std::max(r->cus, 1u));
         int rc2 = ensure(r->wave_trace, words);
         if (rc2) return rc2;
         HIP_TRY(hipMemsetAsync(r->wave_trace.ptr, 0, words * sizeof(unsigned long long), r->stream));

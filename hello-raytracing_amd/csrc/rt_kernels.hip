@@ -172,6 +172,8 @@ struct Tally {
     // diagnostic build, k_trace_split: lane and wave counts of walk steps (internal node / leaf), rounds,
     // lanes shading per round, rounds with a shading lane
     uint32_t lbox = 0, wbox = 0, lleaf = 0, wleaf = 0, rounds = 0, lshade = 0, wshade = 0;
+    // lanes / waves per outer walk iteration (descent + leaf + pop) and lanes walking when the walk is entered
+    uint32_t lwalk = 0, wwalk = 0, lentry = 0;
 #endif
 };
 
@@ -390,7 +392,16 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
         // descent as a bottom-tested loop: one exit (a miss, or a leaf reached) and the node / stack depth updated
         // in place, where the top-tested form below kept two loop-header copies and more exec-mask bookkeeping
         // per box step (C3 +3.2 %). Same visits in the same order (the child order is the three-way form's).
+#ifdef HRT_STAMPS
+        if constexpr (SUSPEND) tally.lentry++;
+#endif
         while (true) {
+#ifdef HRT_STAMPS
+            if constexpr (SUSPEND) {
+                tally.lwalk++;
+                if (first_active_lane()) tally.wwalk++;
+            }
+#endif
             if (!(node & BVH_LEAF_BIT)) {
                 bool any;
                 do {
@@ -2215,7 +2226,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // five PCG steps. (Two float4 per lane before round 4: the bytes saved hold the whole heap top.)
 struct BlockState {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+#ifdef HRT_STAMPS
+    uint32_t nblocks = 0;  // (diagnostic build: frame blocks this wave generated, for its wave record)
+#endif
 };
+
+#ifdef HRT_STAMPS
+// Diagnostic build: the persistent kernels' per-wave record (rt_get_wave_trace; scripts/wave_tail.py), 4 words per wave
+// at wave id blockIdx.x * waves per workgroup + wave: start and end (100 MHz ticks, s_memrealtime), HW_ID | XCC_ID << 32,
+// and (ticks from start until the wave first found no frame block left to take) | frame blocks it generated << 32.
+struct WaveRecord {
+    unsigned long long start = 0, drained = 0;
+    __device__ void begin() { start = hrt_realtime(); }
+    __device__ void drain(bool d) {
+        if (d && drained == 0ull) drained = hrt_realtime() - start;
+    }
+    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks) {
+        if (lane != 0u || P.wave_trace == nullptr) return;
+        const unsigned long long end = hrt_realtime();
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const size_t wid = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        unsigned long long* rec = P.wave_trace + 4u * wid;
+        rec[0] = start;
+        rec[1] = end;
+        rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
+    }
+};
+#endif
 
 template <int MODE, bool STEAL, bool SEED>
 __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
@@ -2245,6 +2285,9 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 }
             }
             B.blk_next = 0;
+#ifdef HRT_STAMPS
+            B.nblocks++;
+#endif
             const uint32_t x = (B.job_tile % K->tiles_w) * 8u + (lane & 7u);
             const uint32_t kr = (B.job_tile / K->tiles_w) * 8u + (lane >> 3);
             const uint32_t pok = (x < K->W && kr < K->nrows) ? 1u : 0u;  // ragged edge tiles: no sample
@@ -2402,6 +2445,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     HRT_PHASE_DECL;
+#ifdef HRT_STAMPS
+    WaveRecord wrec;
+    wrec.begin();
+    uint32_t nblocks = 0;
+#endif
     while (true) {
         bool need = !have && !drained;
         unsigned long long m = __ballot(need);
@@ -2423,6 +2471,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     }
                 }
                 blk_next = 0;
+#ifdef HRT_STAMPS
+                nblocks++;
+#endif
                 const uint32_t x = (job_tile % P.tiles_w) * 8u + (lane & 7u);
                 const uint32_t kr = (job_tile / P.tiles_w) * 8u + (lane >> 3);
                 const uint32_t pok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
@@ -2468,6 +2519,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             if (blk_next == 64u && blk_f + 1u >= job_nf) job_close(J, lane);
             m = __ballot(need);
         }
+#ifdef HRT_STAMPS
+        wrec.drain(drained);
+#endif
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
@@ -2530,18 +2584,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         job_account<1>(J, fin, fl, lane);
         HRT_PHASE(3);
     }
+#ifdef HRT_STAMPS
+    wrec.finish(P, lane, nblocks);
+#endif
     HRT_PHASE_FLUSH
 #if defined(HRT_STAMPS) && !defined(HRT_PHASES)
     {
-        unsigned long long v[7] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
-                                   tally.wshade};
+        unsigned long long v[10] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.rounds, tally.lshade,
+                                    tally.wshade, tally.lwalk, tally.wwalk, tally.lentry};
 #pragma unroll
-        for (int c = 0; c < 7; c++) {
+        for (int c = 0; c < 10; c++) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
         }
         if (lane == 0)
-            for (int c = 0; c < 7; c++) atomicAdd(P.counter + 5 + c, v[c]);
+            for (int c = 0; c < 10; c++) atomicAdd(P.counter + 5 + c, v[c]);  // counters 5-14 ([15] is the job queue)
     }
 #endif
 #ifdef HRT_RINGSTAT
@@ -2634,9 +2691,16 @@ k_trace_split_tris(const KParams P) {
     int bi = -1;  // sphere winner slot
     HeapWalk W;
     HRT_PHASE_DECL;
+#ifdef HRT_STAMPS
+    WaveRecord wrec;
+    wrec.begin();
+#endif
     while (true) {
         refill_block_lds<MODE, STEAL, SEED>(P, B, J, blk, blk_rows, blk_ok, drained, lane, below, have, qs, ray, att, sky_t, s,
                                             bounce, pix, fl);
+#ifdef HRT_STAMPS
+        wrec.drain(drained);
+#endif
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
             if (!drained && idle_spin(J, lane)) break;  // nothing in flight: the next job waits for its ring slot
@@ -2716,6 +2780,9 @@ k_trace_split_tris(const KParams P) {
         job_account<SCAN == SCAN_BVH ? 1 : 2>(J, fin, fl, lane);
         HRT_PHASE(3);
     }
+#ifdef HRT_STAMPS
+    wrec.finish(P, lane, B.nblocks);
+#endif
     HRT_PHASE_FLUSH
 #ifdef HRT_RINGSTAT
     if (lane == 0)

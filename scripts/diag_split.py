@@ -1,4 +1,4 @@
-"""Lane utilisation of k_trace_split's walk and shading phases (diagnostic build counters 5-11).
+"""Lane utilisation of k_trace_split's walk and shading phases (diagnostic build counters 5-14).
 
 Run on the GPU box after `make -C hello-raytracing_amd diag`:
     HRT_LIB=lib/libhrt_diag.so python scripts/diag_split.py [--suspend 0 8 16 32]
@@ -23,8 +23,10 @@ for sb in a.suspend:
     r.draw_frames(sd.frames, 1000, 10)
     st = r.stats()
     c = r.raw_counters()
-    lbox, wbox, lleaf, wleaf, rounds, lshade, wshade = c[5:12]
+    lbox, wbox, lleaf, wleaf, rounds, lshade, wshade, lwalk, wwalk, lentry = c[5:15]
     print(f"suspend_below {sb:2d}: {st.trace_ms:8.1f} ms  box-step util {lbox / max(64 * wbox, 1):.3f}  "
           f"leaf-step util {lleaf / max(64 * wleaf, 1):.3f}  box steps/query {lbox / st.queries:.2f} "
           f"wave box steps/query {64 * wbox / st.queries:.2f}  leaf {lleaf / st.queries:.2f}/{64 * wleaf / st.queries:.2f}  "
-          f"rounds/query/64 {64 * rounds / st.queries:.3f}  shading lanes/round {lshade / max(wshade, 1):.1f}", flush=True)
+          f"rounds/query/64 {64 * rounds / st.queries:.3f}  shading lanes/round {lshade / max(wshade, 1):.1f}  "
+          f"walking lanes per walk iteration {lwalk / max(wwalk, 1):.1f}  lanes entering the walk per round "
+          f"{lentry / max(rounds, 1):.1f}", flush=True)

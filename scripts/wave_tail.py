@@ -1,0 +1,101 @@
+"""Where a short launch loses its time: per-wave records of the suspendable-walk kernels (diagnostic build).
+
+Run on the GPU box after `make -C hello-raytracing_amd diag`:
+    HRT_LIB=lib/libhrt_diag.so python scripts/wave_tail.py --config c4 --ranks 8 --rank 4
+
+Draws one rank's share of the N-way row split (bench.py's partition) and the full image with the bench's timed knobs,
+and summarises each draw's LAST trace launch from its wave records (rt_get_wave_trace): launch span, when waves
+started and when they first found no frame block left (the queue drain), their end times, the resident waves over
+time, and frame blocks per wave. Tells a launch's fixed costs (ramp, drain tail) from a slower per-ray rate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "hello-raytracing_amd"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import bench  # noqa: E402
+import hrt  # noqa: E402
+import scenes  # noqa: E402
+from hrt.parallel import rank_params  # noqa: E402
+
+
+def summarise(tr: np.ndarray) -> dict:
+    st, en = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64)
+    ok = en > 0
+    st, en, info = st[ok], en[ok], tr[ok, 3].astype(np.int64)
+    drained = info & 0xFFFFFFFF
+    blocks = info >> 32
+    t0 = st.min()
+    span = (en.max() - t0) / 1e5
+    pct = lambda a: [round(float(np.percentile(a, q)), 3) for q in (0, 10, 50, 90, 100)]  # noqa: E731
+    edges = np.linspace(t0, en.max(), 26)
+    conc = []
+    for k in range(25):
+        a, b = edges[k], edges[k + 1]
+        conc.append(round(float(np.clip(np.minimum(en, b) - np.maximum(st, a), 0, None).sum() / (b - a)), 1))
+    return {
+        "waves": int(ok.sum()),
+        "span_ms": round(float(span), 3),
+        "start_ms_pcts": pct((st - t0) / 1e5),
+        "drain_ms_pcts": pct((st + drained - t0) / 1e5),
+        "end_ms_pcts": pct((en - t0) / 1e5),
+        "tail_after_first_drain_ms": round(float((en.max() - (st + drained).min()) / 1e5), 3),
+        "blocks_per_wave_pcts": pct(blocks),
+        "blocks_total": int(blocks.sum()),
+        "resident_waves_timeline": conc,
+    }
+
+
+def draw(sd, params: dict):
+    r = scenes.make_renderer(sd)
+    r.set_params(**params)
+    for _ in range(2):  # warm, then the recorded draw
+        r.reset_frame_count()
+        r.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
+        r.synchronize()
+    t = time.perf_counter()
+    r.reset_frame_count()
+    r.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
+    st = r.stats()
+    wall = time.perf_counter() - t
+    import ctypes as C
+    words = 4 * 32 * 256
+    buf = (C.c_uint64 * words)()
+    hrt._lib.check(hrt.lib().rt_get_wave_trace(r._h, buf, words), "rt_get_wave_trace")
+    tr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    out = {"kernel": st.kernel.decode(), "trace_ms": round(st.trace_ms, 3), "kernel_ms": round(st.kernel_ms, 3),
+           "wall_ms": round(wall * 1e3, 3), "trace_launches": st.trace_launches, "rays": st.queries}
+    out.update(summarise(tr))
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--rank", type=int, nargs="+", default=[4])
+    ap.add_argument("--steal", type=int, default=None)
+    ap.add_argument("--full", action="store_true", help="also the full image")
+    a = ap.parse_args()
+    assert hrt.lib().rt_diagnostic_build() == 1, "run with HRT_LIB=lib/libhrt_diag.so"
+    sd = scenes.CONFIGS[a.config]()
+    extra = {} if a.steal is None else {"steal": a.steal}
+    res = {}
+    for k in a.rank:
+        res[f"rank{k}of{a.ranks}"] = draw(sd, {**rank_params(k, a.ranks, 8), **bench.timed_knobs(**extra)})
+    if a.full:
+        res["full"] = draw(sd, {**rank_params(0, 1, 8), **bench.timed_knobs(**extra)})
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
