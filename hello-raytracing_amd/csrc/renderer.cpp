@@ -164,6 +164,7 @@ struct rt_renderer {
     DevBuf<float> nodes_so;  // the same nodes as (lo, hi, lo) per axis (pack_nodes_so)
     bool so_ok = false;
     DevBuf<hrt_dev::TriDev> tris;
+    DevBuf<float> tri_geo;  // a | e1 | e2 per triangle, 9 floats (the deferred tests' operands; KParams::tri_geo)
     DevBuf<hrt_dev::MatDev> mats;
     uint32_t bvh_n = 0, bvh_m = 0;
     // opt-in SAH triangle tree, built on first use after rt_set_bvh
@@ -203,7 +204,8 @@ struct rt_renderer {
     uint32_t row_block() const { return std::max(params.row_block, 1u); }
     uint64_t device_bytes() const {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
-               bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() + mats.bytes() +
+               bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
+               tri_geo.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes();
     }
@@ -501,6 +503,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.so_ok = r->so_ok ? 1u : 0u;
     P.count_tests = r->params.count_tests;
     P.tris = r->tris.ptr;
+    P.tri_geo = r->tri_geo.ptr;
     P.tri_bvh = (r->mode != RT_MODE_SPHERE && r->params.tri_bvh) ? 1u : 0u;
     if (P.tri_bvh) {
         rc = upload_tri_tree(r);
@@ -540,7 +543,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     // fp16 boxes reach up to one half ulp (2^-11 relative) past the f32 root box
     P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
     P.bvh_nnodes = (uint32_t)B.nodes.size();
-    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH) ? 1u : 0u;
+    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH &&
+                    (!hrt_dev::LSPH || B.slot.size() <= hrt_dev::LSPH_CAP)) ? 1u : 0u;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;
@@ -710,7 +714,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             // whole chunks only; tail_split 1 turns it off)
             P.tail_from = 0xFFFFFFFFu;
             P.tail_shift = r->params.tail_split == 3u ? 3u : 2u;
-            if (split && P.suspend_below > 0u && !P.ring_mode && !P.steal && P.job_frames % (1u << P.tail_shift) == 0u &&
+            // (and k_trace's frame-block refill: the simple sphere scan, C2 — round 5, no spills with the decode)
+            const bool tail_kernel = (split && P.suspend_below > 0u) ||
+                                     (r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_SIMPLE);
+            if (tail_kernel && !P.ring_mode && !P.steal && P.job_frames % (1u << P.tail_shift) == 0u &&
                 P.nframes % P.job_frames == 0u && r->params.tail_split != 1u && P.njobs < (1ull << 29)) {
                 const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
                 P.tail_from = (uint32_t)(P.njobs - q);
@@ -836,6 +843,7 @@ void delete_buffers(rt_renderer* r) {
     r->nodes.release();
     r->nodes_so.release();
     r->tris.release();
+    r->tri_geo.release();
     r->mats.release();
     r->tb_hnodes.release();
     r->tb_order.release();
@@ -1037,12 +1045,16 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     int rc = ensure(r->nodes, 2 * (size_t)std::max<uint32_t>(n, 1));
     if (!rc && want_so) rc = ensure(r->nodes_so, so.size());
     if (!rc) rc = ensure(r->tris, std::max<uint32_t>(m, 1));
+    if (!rc) rc = ensure(r->tri_geo, 9 * (size_t)std::max<uint32_t>(m, 1));
     if (!rc) rc = ensure(r->mats, std::max<uint32_t>(n_mats, 1));
     if (rc) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(r->nodes.ptr, nodes32, (size_t)n * 32u, hipMemcpyHostToDevice, r->stream));
     if (want_so)
         HIP_TRY(hipMemcpyAsync(r->nodes_so.ptr, so.data(), so.size() * sizeof(float), hipMemcpyHostToDevice, r->stream));
     if (m) HIP_TRY(hipMemcpyAsync(r->tris.ptr, td.data(), (size_t)m * sizeof(td[0]), hipMemcpyHostToDevice, r->stream));
+    if (m)  // (tri_aee: the same a, e1, e2 floats, 9 per triangle)
+        HIP_TRY(hipMemcpyAsync(r->tri_geo.ptr, r->tri_aee.data(), r->tri_aee.size() * sizeof(float), hipMemcpyHostToDevice,
+                               r->stream));
     if (n_mats)
         HIP_TRY(hipMemcpyAsync(r->mats.ptr, md.data(), (size_t)n_mats * sizeof(md[0]), hipMemcpyHostToDevice, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));

@@ -362,10 +362,12 @@ __device__ __forceinline__ bool box_hit_so(uint32_t px, uint32_t py, uint32_t pz
 // pending sibling per level above it), so a push at an internal node (d <= depth - 1) leaves at most depth. The
 // push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
 // SO (with H16; Q from bvh_begin<.., SO>): box_hit_so.
+// LS_SPH: the leaf spheres from LDS (`ls`, the bvh_sph array copied per workgroup; k_trace_split with HRT_LSPH)
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
-          bool NOOVF = false, bool SO = false, bool COUNT = true>
+          bool NOOVF = false, bool SO = false, bool COUNT = true, bool LS_SPH = false>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
-                                        Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
+                                        Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr,
+                                        const float4* __restrict__ ls = nullptr) {
     static_assert(!SO || H16, "the sign-ordered box test reads fp16 pairs");
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
@@ -437,7 +439,9 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 // one induction variable: the sphere's byte offset (slot word at o / 4, BVH position o / 16)
                 for (uint32_t o = first * 16u, oe = (first + cnt) * 16u; o != oe; o += 16u) {
                     float4 g;
-                    if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
+                    if constexpr (LS_SPH) {
+                        g = ls[o >> 4];
+                    } else if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
                         typedef float f4v __attribute__((ext_vector_type(4)));
                         const __amdgpu_buffer_rsrc_t rs =
                             __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
@@ -798,7 +802,22 @@ __device__ __forceinline__ void tri_record(const KParams& P, const Ray& r, const
 template <bool TBUF = false>
 __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_t j, float& best, int& bj) {
     TriDev tr;
-    if constexpr (TBUF) {  // a, e1, e2 through buffer loads at 32-bit offsets (no 64-bit address per triangle)
+    if constexpr (TBUF) {
+#ifndef HRT_TRI_GEO
+#define HRT_TRI_GEO 1
+#endif
+#if HRT_TRI_GEO
+        // a, e1, e2 from the compact 36-B operand array (tri_geo) through buffer loads at 32-bit offsets
+        typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.tri_geo, (short)0, (int)(P.m * 36u), 0x00020000);
+        const u3v a = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(j * 36u), 0, 0);
+        const u3v e1 = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(j * 36u + 12u), 0, 0);
+        const u3v e2 = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(j * 36u + 24u), 0, 0);
+        tr.a = float4{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), 0.0f};
+        tr.e1 = float4{__uint_as_float(e1.x), __uint_as_float(e1.y), __uint_as_float(e1.z), 0.0f};
+        tr.e2 = float4{__uint_as_float(e2.x), __uint_as_float(e2.y), __uint_as_float(e2.z), 0.0f};
+#else
+        // a, e1, e2 through buffer loads at 32-bit offsets (no 64-bit address per triangle)
         typedef float f4v __attribute__((ext_vector_type(4)));
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.tris, (short)0, (int)(P.m * 64u), 0x00020000);
         const f4v a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j * 64u), 0, 0);
@@ -807,6 +826,7 @@ __device__ __forceinline__ void tri_test(const KParams& P, const Ray& r, uint32_
         tr.a = float4{a.x, a.y, a.z, a.w};
         tr.e1 = float4{e1.x, e1.y, e1.z, e1.w};
         tr.e2 = float4{e2.x, e2.y, e2.z, e2.w};
+#endif
     } else {
         tr = P.tris[j];
     }
@@ -1837,7 +1857,8 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             if (J.dealing()) {
                 B.blk_f++;
             } else {
-                if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
+                // (TAIL: the launch's last jobs in parts, renderer.cpp tail_from; round 5, C2's short launches)
+                if (!job_acquire<true>(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
             }
             B.blk_next = 0;
@@ -2411,18 +2432,25 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // STEAL: frame-block work stealing (sample buffer; renderer.cpp turns it on for launches with few jobs per wave).
 // A separate instantiation: the runtime-switched form cost C3 3 % with stealing off (register allocation).
 template <bool LNODES, bool STEAL, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
+__global__ __launch_bounds__(LNODES ? SPLIT_WG : 256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
+    constexpr uint32_t WG = LNODES ? SPLIT_WG : 256u;  // lanes per workgroup (the LDS stack's lane stride)
+    constexpr bool LSPHK = LNODES && LSPH;             // leaf spheres in LDS (renderer.cpp gates on LSPH_CAP)
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
+    __shared__ uint32_t bvh_stack[SPLIT_STACK * WG];
     __shared__ uint4 lnodes[LNODES ? 2 * LNODE_CAP : 1];
+    __shared__ float4 lsph[LSPHK ? LSPH_CAP : 1];
     if constexpr (LNODES) {
         const uint32_t nn = 2u * min(P.bvh_nnodes, LNODE_CAP);  // renderer.cpp gates LNODES on the same cap
-        for (uint32_t i = threadIdx.x; i < nn; i += 256u) lnodes[i] = P.bvh_hnodes[i];
+        for (uint32_t i = threadIdx.x; i < nn; i += WG) lnodes[i] = P.bvh_hnodes[i];
+        if constexpr (LSPHK) {
+            const uint32_t ns = min(P.bvh_nleaf, LSPH_CAP);
+            for (uint32_t i = threadIdx.x; i < ns; i += WG) lsph[i] = P.bvh_sph[i];
+        }
         __syncthreads();
     }
-    __shared__ float4 blk[2 * 256];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
+    __shared__ float4 blk[2 * WG];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
@@ -2442,7 +2470,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     // once (all lanes busy) into the wave's slice of `blk`, and lanes that need a sample read theirs from
     // it, instead of each freed lane computing its own with a few lanes active.
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
-    __shared__ uint32_t wjobs[4 * WJ_WORDS];
+    __shared__ uint32_t wjobs[(WG / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     HRT_PHASE_DECL;
 #ifdef HRT_STAMPS
@@ -2543,7 +2571,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
             if constexpr (LNODES) {  // (depth <= LNODE_DEPTH = SPLIT_STACK: no overflow)
-                if (bvh_run<true, SPLIT_STACK, true, true, 256, true, true, COUNT>(P, ray, Q, stack, tally, suspend_below, lnodes))
+                if (bvh_run<true, SPLIT_STACK, true, true, WG, true, true, COUNT, LSPHK>(P, ray, Q, stack, tally, suspend_below,
+                                                                                       lnodes, lsph))
                     qs = 2u;
             } else {
                 if (bvh_run<true, SPLIT_STACK, true, true, 256, false, true, COUNT>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
@@ -2994,9 +3023,9 @@ template <bool COUNT>
 static hipError_t launch_trace_split(const KParams& P, hipStream_t stream) {
     const char* base = "k_trace_split";
     if (P.steal)
-        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT))
+        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT), SPLIT_WG)
                             : launch_persistent(k_trace_split<false, true, COUNT>, P, stream, kname_bbb(base, 0, 1, COUNT));
-    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT))
+    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT), SPLIT_WG)
                         : launch_persistent(k_trace_split<false, false, COUNT>, P, stream, kname_bbb(base, 0, 0, COUNT));
 }
 
@@ -3004,7 +3033,9 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     if (P.njobs == 0) return hipSuccess;
     // parts of jobs (tail_from) are decoded by the suspendable-walk kernels with the sample buffer and no stealing only
     // (job_acquire<TAIL>): k_trace_split and k_trace_split_tris (not the opt-in SAH walk's k_trace)
-    const bool split_kernel = mode == MODE_SPHERE ? (variant == SCAN_BVH && P.suspend_below > 0u) : !P.tri_bvh;
+    // (k_trace with the simple sphere scan decodes them in its frame-block refill, refill_block)
+    const bool split_kernel = mode == MODE_SPHERE ? ((variant == SCAN_BVH && P.suspend_below > 0u) || variant == SCAN_SIMPLE)
+                                                  : !P.tri_bvh;
     if (P.tail_from != 0xFFFFFFFFu && !(split_kernel && !P.steal && !P.ring_mode)) return hipErrorInvalidValue;
     switch (mode) {
     case MODE_SPHERE:
