@@ -543,8 +543,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     // fp16 boxes reach up to one half ulp (2^-11 relative) past the f32 root box
     P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
     P.bvh_nnodes = (uint32_t)B.nodes.size();
-    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH &&
-                    (!hrt_dev::LSPH || B.slot.size() <= hrt_dev::LSPH_CAP)) ? 1u : 0u;
+    P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH) ? 1u : 0u;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;

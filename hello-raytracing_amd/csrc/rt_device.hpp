@@ -86,18 +86,6 @@ constexpr uint32_t FOLD_MAX_JOBS = 48;
 
 constexpr uint32_t LNODE_CAP = 192;
 constexpr uint32_t LNODE_DEPTH = 8;
-// k_trace_split<LNODES = true>'s workgroup (HRT_SPLIT_WG lanes; 256 by default) and, with HRT_LSPH, its leaf spheres in
-// LDS too (at most LSPH_CAP; renderer.cpp gates LNODES on it): a larger workgroup shares one copy of the scene among more
-// waves, so 896 lanes (14 waves, two workgroups per CU = 7 waves per SIMD) hold the nodes and the leaf spheres
-#ifndef HRT_SPLIT_WG
-#define HRT_SPLIT_WG 256
-#endif
-#ifndef HRT_LSPH
-#define HRT_LSPH 0
-#endif
-constexpr uint32_t SPLIT_WG = HRT_SPLIT_WG;
-constexpr bool LSPH = HRT_LSPH != 0;
-constexpr uint32_t LSPH_CAP = 512;
 
 // Camera-derived constants of make_ray / fs_main, read only when primary rays are generated (once per frame
 // block in the sample queue). The kernels read them through kargs() (below), a pointer to the kernarg segment

@@ -362,12 +362,10 @@ __device__ __forceinline__ bool box_hit_so(uint32_t px, uint32_t py, uint32_t pz
 // pending sibling per level above it), so a push at an internal node (d <= depth - 1) leaves at most depth. The
 // push then needs no bound check and the walk no overflow flag (5 VALU of a ~50-VALU box step).
 // SO (with H16; Q from bvh_begin<.., SO>): box_hit_so.
-// LS_SPH: the leaf spheres from LDS (`ls`, the bvh_sph array copied per workgroup; k_trace_split with HRT_LSPH)
 template <bool SUSPEND, int STACK = BVH_STACK, bool SELECT = false, bool H16 = false, uint32_t LS = 256,
-          bool NOOVF = false, bool SO = false, bool COUNT = true, bool LS_SPH = false>
+          bool NOOVF = false, bool SO = false, bool COUNT = true>
 __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery& Q, uint32_t* stack,
-                                        Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr,
-                                        const float4* __restrict__ ls = nullptr) {
+                                        Tally& tally, uint32_t below, const uint4* __restrict__ hn = nullptr) {
     static_assert(!SO || H16, "the sign-ordered box test reads fp16 pairs");
     const float4* __restrict__ nodes = P.bvh_nodes;
     const Slab S = Q.S;
@@ -439,9 +437,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 // one induction variable: the sphere's byte offset (slot word at o / 4, BVH position o / 16)
                 for (uint32_t o = first * 16u, oe = (first + cnt) * 16u; o != oe; o += 16u) {
                     float4 g;
-                    if constexpr (LS_SPH) {
-                        g = ls[o >> 4];
-                    } else if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
+                    if constexpr (SELECT) {  // (as below: buffer loads and the fast exact division in k_trace_split)
                         typedef float f4v __attribute__((ext_vector_type(4)));
                         const __amdgpu_buffer_rsrc_t rs =
                             __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
@@ -1726,10 +1722,34 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
 // stealing for < 2^25 - 1 tiles and < 2^11 chunks; claims stop once a slot reads exhausted, so the 16-bit count
 // stays far below its field's end). Wave state in the WaveJobs words the sample buffer leaves unused: flags (own
 // job, queue drained, lost race), the last victim, and the claimed frames not dealt yet.
-constexpr uint32_t STEAL_OWN = 4;
+#ifndef HRT_STEAL_OWN
+#define HRT_STEAL_OWN 4
+#endif
+#ifndef HRT_CLAIM_FREE
+#define HRT_CLAIM_FREE 32
+#endif
+constexpr uint32_t STEAL_OWN = HRT_STEAL_OWN;
 constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u;
+// The tail (round 5): once the job queue is drained, a wave whose lanes are not all free claims another frame block only
+// when at least CLAIM_FREE of them are. A block claimed for a few free lanes waits for this wave's busy ones (paths of
+// up to 50 bounces) while other waves have run dry and exited: C4's 1/8 share drained its queue at 18.1 ms and ran to
+// 23.5 ms (`scripts/wave_tail.py`, profiles/r05/). A wave with every lane free always claims, so the launch drains.
+constexpr uint32_t CLAIM_FREE = HRT_CLAIM_FREE;
+
+
 enum : uint32_t { WJ_ST = WJ_TILE, WJ_VICTIM = WJ_TILE + 1, WJ_PRIV_F = WJ_TILE + 2, WJ_PRIV_N = WJ_TILE + 3,
                   WJ_CLAIM_F = WJ_F0, WJ_CLAIM_T = WJ_LIVE };
+
+// true when the job queue is drained (known to this wave, or read from the queue counter: one load per call)
+__device__ __forceinline__ bool queue_drained(const WaveJobs& J, uint32_t lane) {
+    if (J.get(WJ_ST) & ST_QEMPTY) return true;
+    uint32_t d = 0;
+    if (lane == 0) {
+        const KPtr K = kargs();
+        d = __hip_atomic_load(K->queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= K->njobs ? 1u : 0u;
+    }
+    return uniform(__shfl(d, 0)) != 0u;
+}
 
 __device__ __forceinline__ bool slot_open(unsigned long long w) {
     return (w >> 39) != 0ull && (uint32_t)(w & 0xFFFFu) < (uint32_t)((w >> 16) & 0xFFFu);
@@ -2291,6 +2311,9 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
         if (B.blk_next == 64u) {
             const KPtr K = kargs();  // queue and camera constants: loaded here, not held in SGPRs
             if constexpr (STEAL) {  // one frame block at a time, stolen once the queue is drained (steal_block)
+                if ((uint32_t)__popcll(m) < CLAIM_FREE && J.get(WJ_PRIV_N) == 0u && __ballot(have) != 0ull &&
+                    queue_drained(J, lane))
+                    break;  // (the tail: leave the block to a wave with more free lanes, CLAIM_FREE)
                 if (!steal_block(J, lane, B.job_tile, B.job_f0)) {
                     drained = steal_drained(J);
                     break;
@@ -2432,25 +2455,18 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // STEAL: frame-block work stealing (sample buffer; renderer.cpp turns it on for launches with few jobs per wave).
 // A separate instantiation: the runtime-switched form cost C3 3 % with stealing off (register allocation).
 template <bool LNODES, bool STEAL, bool COUNT>
-__global__ __launch_bounds__(LNODES ? SPLIT_WG : 256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
     constexpr int MODE = MODE_SPHERE;
     constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
-    constexpr uint32_t WG = LNODES ? SPLIT_WG : 256u;  // lanes per workgroup (the LDS stack's lane stride)
-    constexpr bool LSPHK = LNODES && LSPH;             // leaf spheres in LDS (renderer.cpp gates on LSPH_CAP)
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t bvh_stack[SPLIT_STACK * WG];
+    __shared__ uint32_t bvh_stack[SPLIT_STACK * 256];
     __shared__ uint4 lnodes[LNODES ? 2 * LNODE_CAP : 1];
-    __shared__ float4 lsph[LSPHK ? LSPH_CAP : 1];
     if constexpr (LNODES) {
         const uint32_t nn = 2u * min(P.bvh_nnodes, LNODE_CAP);  // renderer.cpp gates LNODES on the same cap
-        for (uint32_t i = threadIdx.x; i < nn; i += WG) lnodes[i] = P.bvh_hnodes[i];
-        if constexpr (LSPHK) {
-            const uint32_t ns = min(P.bvh_nleaf, LSPH_CAP);
-            for (uint32_t i = threadIdx.x; i < ns; i += WG) lsph[i] = P.bvh_sph[i];
-        }
+        for (uint32_t i = threadIdx.x; i < nn; i += 256u) lnodes[i] = P.bvh_hnodes[i];
         __syncthreads();
     }
-    __shared__ float4 blk[2 * WG];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
+    __shared__ float4 blk[2 * 256];  // the wave's frame block: (o.xyz, d.x), (d.yz, state bits, ok) per lane
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
@@ -2470,7 +2486,7 @@ __global__ __launch_bounds__(LNODES ? SPLIT_WG : 256) __attribute__((amdgpu_wave
     // once (all lanes busy) into the wave's slice of `blk`, and lanes that need a sample read theirs from
     // it, instead of each freed lane computing its own with a few lanes active.
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
-    __shared__ uint32_t wjobs[(WG / 64u) * WJ_WORDS];
+    __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     HRT_PHASE_DECL;
 #ifdef HRT_STAMPS
@@ -2484,6 +2500,9 @@ __global__ __launch_bounds__(LNODES ? SPLIT_WG : 256) __attribute__((amdgpu_wave
         while (m != 0ull) {
             if (blk_next == 64u) {
                 if constexpr (STEAL) {  // one frame block at a time, stolen once the queue is drained (steal_block)
+                    if ((uint32_t)__popcll(m) < CLAIM_FREE && J.get(WJ_PRIV_N) == 0u && __ballot(have) != 0ull &&
+                        queue_drained(J, lane))
+                        break;  // (the tail: leave the block to a wave with more free lanes, CLAIM_FREE)
                     if (!steal_block(J, lane, job_tile, job_f0)) {
                         drained = steal_drained(J);
                         break;
@@ -2571,8 +2590,7 @@ __global__ __launch_bounds__(LNODES ? SPLIT_WG : 256) __attribute__((amdgpu_wave
         HRT_LANES(1, have && qs == 1u);
         if (have && qs == 1u) {
             if constexpr (LNODES) {  // (depth <= LNODE_DEPTH = SPLIT_STACK: no overflow)
-                if (bvh_run<true, SPLIT_STACK, true, true, WG, true, true, COUNT, LSPHK>(P, ray, Q, stack, tally, suspend_below,
-                                                                                       lnodes, lsph))
+                if (bvh_run<true, SPLIT_STACK, true, true, 256, true, true, COUNT>(P, ray, Q, stack, tally, suspend_below, lnodes))
                     qs = 2u;
             } else {
                 if (bvh_run<true, SPLIT_STACK, true, true, 256, false, true, COUNT>(P, ray, Q, stack, tally, suspend_below, P.bvh_hnodes))
@@ -3023,9 +3041,9 @@ template <bool COUNT>
 static hipError_t launch_trace_split(const KParams& P, hipStream_t stream) {
     const char* base = "k_trace_split";
     if (P.steal)
-        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT), SPLIT_WG)
+        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT))
                             : launch_persistent(k_trace_split<false, true, COUNT>, P, stream, kname_bbb(base, 0, 1, COUNT));
-    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT), SPLIT_WG)
+    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT))
                         : launch_persistent(k_trace_split<false, false, COUNT>, P, stream, kname_bbb(base, 0, 0, COUNT));
 }
 
