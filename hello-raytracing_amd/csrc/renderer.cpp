@@ -713,10 +713,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             // whole chunks only; tail_split 1 turns it off)
             P.tail_from = 0xFFFFFFFFu;
             P.tail_shift = r->params.tail_split == 3u ? 3u : 2u;
-            // (and k_trace's frame-block refill: the simple sphere scan, C2 — round 5, no spills with the decode)
-            const bool tail_kernel = (split && P.suspend_below > 0u) ||
-                                     (r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_SIMPLE);
-            if (tail_kernel && !P.ring_mode && !P.steal && P.job_frames % (1u << P.tail_shift) == 0u &&
+            // (k_trace's frame-block refill could decode them too, without spills: C2's full image ran 9 % slower with the
+            // parts, 74.1 vs 81.3 Grays/s, for its 8-way split 0.51 -> 0.55; round 5, profiles/r05/f/)
+            if (split && P.suspend_below > 0u && !P.ring_mode && !P.steal && P.job_frames % (1u << P.tail_shift) == 0u &&
                 P.nframes % P.job_frames == 0u && r->params.tail_split != 1u && P.njobs < (1ull << 29)) {
                 const unsigned long long q = std::min<unsigned long long>(P.njobs, 64ull * std::max(r->cus, 1u));
                 P.tail_from = (uint32_t)(P.njobs - q);

@@ -1723,7 +1723,7 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
 // stays far below its field's end). Wave state in the WaveJobs words the sample buffer leaves unused: flags (own
 // job, queue drained, lost race), the last victim, and the claimed frames not dealt yet.
 #ifndef HRT_STEAL_OWN
-#define HRT_STEAL_OWN 4
+#define HRT_STEAL_OWN 1  // (4 before round 5: the owner's claims of 4 frames held them from idle thieves in the tail)
 #endif
 #ifndef HRT_CLAIM_FREE
 #define HRT_CLAIM_FREE 32
@@ -1877,8 +1877,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             if (J.dealing()) {
                 B.blk_f++;
             } else {
-                // (TAIL: the launch's last jobs in parts, renderer.cpp tail_from; round 5, C2's short launches)
-                if (!job_acquire<true>(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
+                if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
             }
             B.blk_next = 0;
@@ -3051,9 +3050,7 @@ hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t
     if (P.njobs == 0) return hipSuccess;
     // parts of jobs (tail_from) are decoded by the suspendable-walk kernels with the sample buffer and no stealing only
     // (job_acquire<TAIL>): k_trace_split and k_trace_split_tris (not the opt-in SAH walk's k_trace)
-    // (k_trace with the simple sphere scan decodes them in its frame-block refill, refill_block)
-    const bool split_kernel = mode == MODE_SPHERE ? ((variant == SCAN_BVH && P.suspend_below > 0u) || variant == SCAN_SIMPLE)
-                                                  : !P.tri_bvh;
+    const bool split_kernel = mode == MODE_SPHERE ? (variant == SCAN_BVH && P.suspend_below > 0u) : !P.tri_bvh;
     if (P.tail_from != 0xFFFFFFFFu && !(split_kernel && !P.steal && !P.ring_mode)) return hipErrorInvalidValue;
     switch (mode) {
     case MODE_SPHERE:
