@@ -1435,7 +1435,7 @@ enum : uint32_t { WJ_TILE = 0, WJ_F0 = WJ_NE, WJ_LIVE = 2 * WJ_NE, WJ_SLOT = 3 *
 // flags: busy bit per entry (bits 0..WJ_NE-1), the current entry (bits 8-9), dealing, waiting
 // (slotted: the waiting current job has its slot)
 enum : uint32_t { WJ_BUSY = (1u << WJ_NE) - 1u, WJ_CUR_SHIFT = 8, WJ_DEALING = 1u << 12, WJ_WAITING = 1u << 13,
-                  WJ_SLOTTED = 1u << 14 };
+                  WJ_SLOTTED = 1u << 14, WJ_TAILPH = 1u << 15 /* the wave has dealt a tail part (TAIL): CLAIM_FREE */ };
 struct WaveJobs {
     uint32_t* w;  // this wave's words
     __device__ uint32_t get(uint32_t i) const { return uniform(w[i]); }
@@ -1627,6 +1627,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
             if (part) {
                 job_nf >>= ts;
                 job_f0 += (q & ((1u << ts) - 1u)) * job_nf;
+                J.set(WJ_FLAGS, flags | WJ_DEALING | WJ_TAILPH);
             }
         } else {
             job_tile = j / K->nchunks;
@@ -1735,6 +1736,12 @@ constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u;
 // up to 50 bounces) while other waves have run dry and exited: C4's 1/8 share drained its queue at 18.1 ms and ran to
 // 23.5 ms (`scripts/wave_tail.py`, profiles/r05/). A wave with every lane free always claims, so the launch drains.
 constexpr uint32_t CLAIM_FREE = HRT_CLAIM_FREE;
+// The same rule for a wave that has dealt a tail part (job_acquire<TAIL>, no stealing): its next part waits for
+// CLAIM_FREE free lanes (HRT_TAIL_CLAIM 0 = round 4: a part for any free lane).
+#ifndef HRT_TAIL_CLAIM
+#define HRT_TAIL_CLAIM 1
+#endif
+constexpr bool TAIL_CLAIM = HRT_TAIL_CLAIM != 0;
 
 
 enum : uint32_t { WJ_ST = WJ_TILE, WJ_VICTIM = WJ_TILE + 1, WJ_PRIV_F = WJ_TILE + 2, WJ_PRIV_N = WJ_TILE + 3,
@@ -2323,6 +2330,8 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
                 if (J.dealing()) {
                     B.blk_f++;
                 } else {
+                    // (the tail: once this wave dealt a tail part, a new one only for CLAIM_FREE free lanes, as stealing)
+                    if (TAIL_CLAIM && (J.get(WJ_FLAGS) & WJ_TAILPH) && (uint32_t)__popcll(m) < CLAIM_FREE && __ballot(have) != 0ull) break;
                     if (!job_acquire<true>(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                     B.blk_f = 0;
                 }
@@ -2512,6 +2521,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     if (J.dealing()) {
                         blk_f++;
                     } else {
+                        // (the tail: once this wave dealt a tail part, a new one only for CLAIM_FREE free lanes, as stealing)
+                        if (TAIL_CLAIM && (J.get(WJ_FLAGS) & WJ_TAILPH) && (uint32_t)__popcll(m) < CLAIM_FREE && __ballot(have) != 0ull)
+                            break;
                         if (!job_acquire<true>(J, lane, drained, job_tile, job_f0, job_nf)) break;
                         blk_f = 0;
                     }

@@ -13,7 +13,7 @@ for cfg in "$@"; do
       tag=$(basename "$lib" .so)
       HRT_LIB="$lib" timeout -k 10 300 python bench.py --config "$cfg" --no-cpu-baseline --no-golden $args \
         > "gpurun_out/ab/${cfg}_$tag.log" 2>&1
-      echo "$cfg $tag $(tail -1 gpurun_out/ab/${cfg}_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+      echo "$cfg $tag $(tail -1 gpurun_out/ab/${cfg}_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); e=d.get('emulated_split') or {}; print(d['value'], d['ms_per_step'], e.get('efficiency', ''), e.get('predicted_ms_per_step', ''))")"
     done
   done
 done
