@@ -482,6 +482,8 @@ def main() -> int:
     ap.add_argument("--steal", type=int, default=None,
                     help="sample queue: frame-block work stealing, 0 auto (short launches), 1 off, 2 on")
     ap.add_argument("--tail-split", type=int, default=None, help="sample queue: 0 auto (quarter jobs at the end), 1 off")
+    ap.add_argument("--cost-order", type=int, default=None,
+                    help="sample queue: 0 auto = deal tiles by the previous launch's cost, most expensive first; 1 off")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -562,6 +564,8 @@ def main() -> int:
         extra["steal"] = args.steal
     if args.tail_split is not None:
         extra["tail_split"] = args.tail_split
+    if args.cost_order is not None:
+        extra["cost_order"] = args.cost_order
     # the timed draws run the default kernels (count_tests 0: the sphere program's k_trace_split does not count its box
     # and sphere tests); the warmup draws count them (count_tests 1) for the per-ray figures of the line, the same
     # every step (bit-identical draws)

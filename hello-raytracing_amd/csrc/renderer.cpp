@@ -25,6 +25,7 @@
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
+hipError_t hrt_launch_order(uint32_t* cost, uint32_t ntiles, uint32_t* order, uint32_t* scratch, hipStream_t stream);
 const char* hrt_last_kernel();
 void hrt_reset_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
@@ -180,6 +181,12 @@ struct rt_renderer {
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
+    // cost-ordered dealing (rt_params.cost_order): per-tile query counts of the last sample-buffer launch, the tile
+    // order built from them for the next one, the counting sort's histogram / cursors; cost_tiles: the tile count
+    // they were set up for, order_tiles: the tile count tile_order holds a permutation of (0: none yet)
+    DevBuf<uint32_t> tile_cost, tile_order, order_scratch;
+    uint32_t cost_tiles = 0, order_tiles = 0;
+    uint32_t last_ordered = 0;  // trace launches of the last sample-queue draw that dealt in cost order
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
 
@@ -207,7 +214,7 @@ struct rt_renderer {
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
                tri_geo.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
-               wave_trace.bytes() + steal_slots.bytes();
+               wave_trace.bytes() + steal_slots.bytes() + tile_cost.bytes() + tile_order.bytes() + order_scratch.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
@@ -556,7 +563,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->last_schedule = schedule;
     r->last_suspend = 0;
 
-    uint32_t launches = 0;
+    uint32_t launches = 0, ordered = 0;
     hrt_reset_last_kernel();  // (a draw that launches nothing reports no kernel)
     if (P.nrows == 0u) {  // a renderer that owns no rows (row0 at or below the last row): nothing to trace
         r->trace_pairs = 0;
@@ -685,6 +692,22 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         rc = ensure(r->steal_slots, P.steal_cap);
         if (rc) return rc;
         P.steal_slots = r->steal_slots.ptr;
+        // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): every sample-buffer launch sums its
+        // samples' queries per tile, and the next launch (of this draw or the next) deals the tiles most expensive
+        // first, so the jobs that take longest start first instead of trailing the launch. Bit-identical in any order.
+        const bool cost_on = !P.ring_mode && r->params.cost_order != 1u;
+        if (cost_on && r->cost_tiles != ntiles) {
+            constexpr size_t SCRATCH = 2u * 128u;  // 2 x ORDER_BUCKETS
+            rc = ensure(r->tile_cost, ntiles);
+            if (!rc) rc = ensure(r->tile_order, ntiles);
+            if (!rc) rc = ensure(r->order_scratch, SCRATCH);
+            if (rc) return rc;
+            HIP_TRY(hipMemsetAsync(r->tile_cost.ptr, 0, (size_t)ntiles * sizeof(uint32_t), r->stream));
+            HIP_TRY(hipMemsetAsync(r->order_scratch.ptr, 0, SCRATCH * sizeof(uint32_t), r->stream));
+            r->cost_tiles = ntiles;
+            r->order_tiles = 0;
+        }
+        P.tile_cost = cost_on ? r->tile_cost.ptr : nullptr;
         P.queue = r->counter.ptr + 15u;
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
@@ -728,16 +751,23 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             rc = trace_events(r, r->trace_pairs_pending);
             if (rc) return rc;
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
+            P.tile_order = cost_on && r->order_tiles == ntiles ? r->tile_order.ptr : nullptr;
+            ordered += P.tile_order ? 1u : 0u;
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
             r->trace_pairs_pending++;
             launches++;
+            if (cost_on) {  // (three small kernels, not counted in rt_stats.launches)
+                HIP_TRY(hrt_launch_order(r->tile_cost.ptr, ntiles, r->tile_order.ptr, r->order_scratch.ptr, r->stream));
+                r->order_tiles = ntiles;
+            }
             if (!P.ring_mode) {
                 HIP_TRY(hrt_launch_accumulate(P, r->stream));
                 launches++;
             }
         }
         r->last_launch_frames = chunk;
+        r->last_ordered = ordered;
         r->trace_pairs = r->trace_pairs_pending;
         r->trace_pairs_pending = 0;
     } else {
@@ -763,6 +793,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         r->stats.fold_ring = P.ring_mode;
         r->stats.fold_bytes = r->fold_bytes;
         r->stats.launch_frames = std::min(count, r->last_launch_frames);
+        r->stats.ordered_launches = r->last_ordered;
     }
     r->stats.device_bytes = r->device_bytes();
     r->timing_pending = true;
@@ -851,6 +882,10 @@ void delete_buffers(rt_renderer* r) {
     r->ring.release();
     r->ring_ctl.release();
     r->wave_trace.release();
+    r->tile_cost.release();
+    r->tile_order.release();
+    r->order_scratch.release();
+    r->cost_tiles = r->order_tiles = 0;
 }
 
 }  // namespace
@@ -963,6 +998,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
     if (p->count_tests > 1) return fail(RT_ERR_ARG, "rt_set_params: count_tests must be 0 or 1");
+    if (p->cost_order > 2) return fail(RT_ERR_ARG, "rt_set_params: cost_order must be 0 auto, 1 off or 2 on");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

@@ -174,6 +174,9 @@ struct Tally {
     uint32_t lbox = 0, wbox = 0, lleaf = 0, wleaf = 0, rounds = 0, lshade = 0, wshade = 0;
     // lanes / waves per outer walk iteration (descent + leaf + pop) and lanes walking when the walk is entered
     uint32_t lwalk = 0, wwalk = 0, lentry = 0;
+    // the mixed kernel's run-to-completion sphere walk (k_trace_split_tris, begin phase): walks entered (waves), and the
+    // box / leaf steps run with fewer than DIAG_LOW lanes (waves, lanes)
+    uint32_t wentry = 0, wbox_low = 0, lbox_low = 0, wleaf_low = 0, lleaf_low = 0;
 #endif
 };
 
@@ -393,22 +396,27 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
         // in place, where the top-tested form below kept two loop-header copies and more exec-mask bookkeeping
         // per box step (C3 +3.2 %). Same visits in the same order (the child order is the three-way form's).
 #ifdef HRT_STAMPS
-        if constexpr (SUSPEND) tally.lentry++;
+        tally.lentry++;
+        if (first_active_lane()) tally.wentry++;
 #endif
         while (true) {
 #ifdef HRT_STAMPS
-            if constexpr (SUSPEND) {
-                tally.lwalk++;
-                if (first_active_lane()) tally.wwalk++;
-            }
+            tally.lwalk++;
+            if (first_active_lane()) tally.wwalk++;
 #endif
             if (!(node & BVH_LEAF_BIT)) {
                 bool any;
                 do {
 #ifdef HRT_STAMPS
-                    if constexpr (SUSPEND) {
+                    {
+                        constexpr uint32_t DIAG_LOW = 24u;
+                        const bool low = (uint32_t)__popcll(__ballot(1)) < DIAG_LOW;
                         tally.lbox++;
-                        if (first_active_lane()) tally.wbox++;
+                        tally.lbox_low += low ? 1u : 0u;
+                        if (first_active_lane()) {
+                            tally.wbox++;
+                            tally.wbox_low += low ? 1u : 0u;
+                        }
                     }
 #endif
                     float tl, tr;
@@ -427,9 +435,15 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
             }
             if (node & BVH_LEAF_BIT) {
 #ifdef HRT_STAMPS
-                if constexpr (SUSPEND) {
+                {
+                    constexpr uint32_t DIAG_LOW = 24u;
+                    const bool low = (uint32_t)__popcll(__ballot(1)) < DIAG_LOW;
                     tally.lleaf++;
-                    if (first_active_lane()) tally.wleaf++;
+                    tally.lleaf_low += low ? 1u : 0u;
+                    if (first_active_lane()) {
+                        tally.wleaf++;
+                        tally.wleaf_low += low ? 1u : 0u;
+                    }
                 }
 #endif
                 const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
@@ -1451,7 +1465,8 @@ __device__ __forceinline__ uint32_t sample_ref(const WaveJobs& J, uint32_t f0, u
     return kargs()->ring_mode ? (J.cur() << 16) | fj : f0 + fj;
 }
 
-__device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint32_t ref, const f3 c) {
+// cost: the sample's queries (its tile's cost for the next launch's deal order, cost-ordered dealing)
+__device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint32_t ref, const f3 c, uint32_t cost) {
     const KPtr K = kargs();
     if (!K->ring_mode) {  // sample buffer: the colour at its frame of the launch, folded by k_accumulate
         const uint32_t npix = K->tiles_w * K->tiles_h * 64u;  // tile-padded pixels of a frame (< 2^32)
@@ -1459,6 +1474,7 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
         o[0] = c.x;
         o[1] = c.y;
         o[2] = c.z;
+        if (uint32_t* const tc = K->tile_cost) __hip_atomic_fetch_add(tc + (pix >> 6), cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     const uint32_t slot = J.w[WJ_SLOT + (ref >> 16)];  // per-lane entry: an LDS read, not a uniform value
@@ -1623,6 +1639,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
             const uint32_t jj = part ? tail + (q >> ts) : j;
             job_tile = jj / K->nchunks;
             job_f0 = (jj - job_tile * K->nchunks) * K->job_frames;
+            if (const uint32_t* const ord = K->tile_order) job_tile = ord[job_tile];
             job_nf = min(K->job_frames, K->nframes - job_f0);
             if (part) {
                 job_nf >>= ts;
@@ -1632,6 +1649,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
         } else {
             job_tile = j / K->nchunks;
             job_f0 = (j % K->nchunks) * K->job_frames;
+            if (const uint32_t* const ord = K->tile_order) job_tile = ord[job_tile];
             job_nf = min(K->job_frames, K->nframes - job_f0);
         }
         return true;
@@ -1838,7 +1856,8 @@ __device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t la
             const uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
             unsigned long long v = 0;
             if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
-                const uint32_t t = j / K->nchunks, c = j - t * K->nchunks;
+                const uint32_t tj = j / K->nchunks, c = j - tj * K->nchunks;
+                const uint32_t t = K->tile_order ? K->tile_order[tj] : tj;
                 const uint32_t nf = min(K->job_frames, K->nframes - c * K->job_frames);
                 v = ((unsigned long long)(t + 1u) << 39) | ((unsigned long long)c << 28) | ((unsigned long long)nf << 16);
                 (void)atomicExch(slots + wid, v + STEAL_OWN);
@@ -2089,6 +2108,32 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // completes a tile's last job folds the slot into the image in frame order per pixel with the reference's
 // mix (shader_sphere.wgsl:264-271; fold_session), so the image is bit-identical to k_render's and to
 // count x rt_draw.
+#ifdef HRT_STAMPS
+// Diagnostic build: the persistent kernels' per-wave record (rt_get_wave_trace; scripts/wave_tail.py), 4 words per wave
+// at wave id blockIdx.x * waves per workgroup + wave: start and end (100 MHz ticks, s_memrealtime), HW_ID | XCC_ID << 32,
+// and (ticks from start until the wave first found no frame block left to take) | frame blocks it generated << 32.
+struct WaveRecord {
+    unsigned long long start = 0, drained = 0;
+    __device__ void begin() { start = hrt_realtime(); }
+    __device__ void drain(bool d) {
+        if (d && drained == 0ull) drained = hrt_realtime() - start;
+    }
+    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks) {
+        if (lane != 0u || P.wave_trace == nullptr) return;
+        const unsigned long long end = hrt_realtime();
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const size_t wid = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        unsigned long long* rec = P.wave_trace + 4u * wid;
+        rec[0] = start;
+        rec[1] = end;
+        rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
+    }
+};
+#endif
+
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
 // (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
@@ -2120,6 +2165,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     unsigned long long st_pq = 0, st_pbox = 0, st_ptrav = 0;
     const unsigned long long st_start = hrt_stamp();
     const unsigned long long rt_start = hrt_realtime();
+    WaveRecord wrec;
+    wrec.begin();
 #endif
     while (true) {
 #ifdef HRT_STAMPS
@@ -2176,6 +2223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #ifdef HRT_STAMPS
         st_tb = hrt_stamp();
         if (have) st_gen += st_tb - st_ta;
+        wrec.drain(drained);
 #endif
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
@@ -2212,7 +2260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             const float u = 1.0f - sky_t;
             const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
             const f3 c = att * sky;
-            ring_store(J, pix, fl, c);
+            ring_store(J, pix, fl, c, bounce + 1u);
             have = false;
             fin = true;
         }
@@ -2222,6 +2270,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
+    wrec.finish(P, lane, 0u);
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)
@@ -2278,31 +2327,6 @@ struct BlockState {
 #endif
 };
 
-#ifdef HRT_STAMPS
-// Diagnostic build: the persistent kernels' per-wave record (rt_get_wave_trace; scripts/wave_tail.py), 4 words per wave
-// at wave id blockIdx.x * waves per workgroup + wave: start and end (100 MHz ticks, s_memrealtime), HW_ID | XCC_ID << 32,
-// and (ticks from start until the wave first found no frame block left to take) | frame blocks it generated << 32.
-struct WaveRecord {
-    unsigned long long start = 0, drained = 0;
-    __device__ void begin() { start = hrt_realtime(); }
-    __device__ void drain(bool d) {
-        if (d && drained == 0ull) drained = hrt_realtime() - start;
-    }
-    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks) {
-        if (lane != 0u || P.wave_trace == nullptr) return;
-        const unsigned long long end = hrt_realtime();
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        const size_t wid = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        unsigned long long* rec = P.wave_trace + 4u * wid;
-        rec[0] = start;
-        rec[1] = end;
-        rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
-        rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
-    }
-};
-#endif
 
 template <int MODE, bool STEAL, bool SEED>
 __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
@@ -2633,7 +2657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                ring_store(J, pix, fl, c);
+                ring_store(J, pix, fl, c, bounce + 1u);
                 have = false;
                 fin = true;
             }
@@ -2829,7 +2853,7 @@ k_trace_split_tris(const KParams P) {
                 const float u = 1.0f - sky_t;
                 const f3 sky = mk(0.54f * u + 0.54f * sky_t, 0.86f * u + 0.7f * sky_t, 0.92f * u + 0.98f * sky_t);
                 const f3 c = att * sky;
-                ring_store(J, pix, fl, c);
+                ring_store(J, pix, fl, c, bounce + 1u);
                 have = false;
                 fin = true;
             }
@@ -2840,6 +2864,20 @@ k_trace_split_tris(const KParams P) {
     }
 #ifdef HRT_STAMPS
     wrec.finish(P, lane, B.nblocks);
+#ifndef HRT_PHASES
+    {
+        // the begin phase's sphere walk (scripts/diag_tris.py): counter[5..14]
+        unsigned long long v[10] = {tally.lbox, tally.wbox, tally.lleaf, tally.wleaf, tally.lbox_low, tally.wbox_low,
+                                    tally.lleaf_low, tally.wleaf_low, tally.lentry, tally.wentry};
+#pragma unroll
+        for (int c = 0; c < 10; c++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
+        }
+        if (lane == 0)
+            for (int c = 0; c < 10; c++) atomicAdd(P.counter + 5 + c, v[c]);
+    }
+#endif
 #endif
     HRT_PHASE_FLUSH
 #ifdef HRT_RINGSTAT
@@ -2880,6 +2918,62 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
     const size_t npad = (size_t)P.tiles_w * P.tiles_h * 64u;
     if (npad == 0 || P.nframes == 0) return hipSuccess;
     hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npad + 255u) / 256u)), dim3(256), 0, stream, P);
+    return hipGetLastError();
+}
+
+// Cost-ordered dealing (rt_params.cost_order; renderer.cpp): after a sample-buffer launch the tiles are ordered by the
+// queries their samples took in it (tile_cost, summed by ring_store), most expensive first, and the next launch deals
+// its jobs in that tile order (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths stay in
+// glass for the bounce cap costs ~25x a sky tile; dealt late, its jobs outlast the launch (C4's 1/8 share: queue
+// drained at 17 ms, last wave at 38 ms without stealing, 21.5 with it). The order is a counting sort on ORDER_BUCKETS
+// log-scale cost classes (4 per octave; order within a class is arbitrary): which wave traces a sample never changes
+// its colour or its place in the sample buffer, so the image is bit-identical in any order.
+constexpr uint32_t ORDER_BUCKETS = 128;
+__device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
+    // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, < 2^32: < 128),
+    // most expensive first
+    const uint32_t k = (__float_as_uint((float)cost + 1.0f) >> 21) - (127u << 2);
+    return (ORDER_BUCKETS - 1u) - min(k, ORDER_BUCKETS - 1u);
+}
+__global__ __launch_bounds__(256) void k_order_hist(const uint32_t* __restrict__ cost, uint32_t ntiles, uint32_t* hist) {
+    __shared__ uint32_t h[ORDER_BUCKETS];
+    for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) h[b] = 0u;
+    __syncthreads();
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < ntiles; t += gridDim.x * 256u) atomicAdd(&h[order_bucket(cost[t])], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u)
+        if (h[b]) atomicAdd(hist + b, h[b]);
+}
+// one workgroup: hist -> exclusive prefix sums (the classes' first positions) in cursor, hist zeroed for the next launch
+__global__ __launch_bounds__(ORDER_BUCKETS) void k_order_scan(uint32_t* hist, uint32_t* cursor) {
+    __shared__ uint32_t v[ORDER_BUCKETS];
+    const uint32_t b = threadIdx.x;
+    v[b] = hist[b];
+    hist[b] = 0u;
+    __syncthreads();
+    for (uint32_t o = 1; o < ORDER_BUCKETS; o <<= 1) {
+        const uint32_t add = b >= o ? v[b - o] : 0u;
+        __syncthreads();
+        v[b] += add;
+        __syncthreads();
+    }
+    cursor[b] = b ? v[b - 1u] : 0u;
+}
+__global__ __launch_bounds__(256) void k_order_scatter(uint32_t* cost, uint32_t ntiles, uint32_t* cursor, uint32_t* order) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint32_t pos = atomicAdd(cursor + order_bucket(cost[t]), 1u);
+    order[pos] = t;
+    cost[t] = 0u;  // the next launch's costs
+}
+// scratch: 2 * ORDER_BUCKETS words, zero on the first call (k_order_scan leaves the histogram zeroed)
+hipError_t hrt_launch_order(uint32_t* cost, uint32_t ntiles, uint32_t* order, uint32_t* scratch, hipStream_t stream) {
+    if (ntiles == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint32_t>((ntiles + 255u) / 256u, 1024u);
+    hipLaunchKernelGGL(k_order_hist, dim3(blocks), dim3(256), 0, stream, cost, ntiles, scratch);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_BUCKETS), 0, stream, scratch, scratch + ORDER_BUCKETS);
+    hipLaunchKernelGGL(k_order_scatter, dim3((ntiles + 255u) / 256u), dim3(256), 0, stream, cost, ntiles,
+                       scratch + ORDER_BUCKETS, order);
     return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ class RtParams(C.Structure):
         ("steal", C.c_uint32),
         ("tail_split", C.c_uint32),
         ("count_tests", C.c_uint32),
+        ("cost_order", C.c_uint32),
     ]
 
 
@@ -74,6 +75,8 @@ class RtStats(C.Structure):
         ("fold_ring", C.c_uint32),
         ("launch_frames", C.c_uint32),
         ("device_bytes", C.c_uint64),
+        ("ordered_launches", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

@@ -115,6 +115,11 @@ typedef struct rt_params {
                                   (rt_stats.box_tests / sphere_tests); 0 (default): the sphere program's
                                   k_trace_split does not count them (reported 0; 1.3 % of C3's kernel
                                   time); the other kernels always count                                  */
+    uint32_t cost_order;       /* sample queue with the sample buffer: deal each launch's tiles in descending
+                                  order of the queries their samples took in the renderer's previous launch
+                                  (of this draw or an earlier one with the same tile count), so the slowest
+                                  jobs start first; the first launch deals in raster order. 0 auto = on,
+                                  1 off, 2 on; bit-identical always               */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u
@@ -152,6 +157,9 @@ typedef struct rt_stats {
                               have fewer; rt_params.queue_budget_mb)                                   */
     uint64_t device_bytes; /* device memory the renderer holds after the last draw call (image, scene,
                               colour fold, counters): the fold's share stays within queue_budget_mb      */
+    uint32_t ordered_launches; /* trace launches of the last draw that dealt their tiles in cost order
+                              (rt_params.cost_order)                                                    */
+    uint32_t reserved;
 } rt_stats;
 
 /* Renderer::new(RenderOutput::Headless(w, h), ..) — renderer.rs:46-269. Zeroes the image (:249-257),

@@ -104,8 +104,8 @@ def test_struct_layouts_match_header():
         got = [(f, t) for f, t in py._fields_]
         assert [f for f, _ in fields] == [f for f, _ in got], name
         assert [C.sizeof(t) for _, t in fields] == [C.sizeof(t) for _, t in got], name
-    assert C.sizeof(hrt.RtParams) == 18 * 4
-    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64 + 8 + 4 + 4 + 8
+    assert C.sizeof(hrt.RtParams) == 19 * 4
+    assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64 + 8 + 4 + 4 + 8 + 4 + 4
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(6)] == [80, 32, 48, 32, 64, C.sizeof(O.OParams)]
 
