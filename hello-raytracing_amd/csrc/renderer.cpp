@@ -25,7 +25,8 @@
 hipError_t hrt_launch_render(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
-hipError_t hrt_launch_order(uint32_t* cost, uint32_t ntiles, uint32_t* order, uint32_t* scratch, hipStream_t stream);
+hipError_t hrt_launch_order(uint32_t* pixel_cost, uint32_t ntiles, uint32_t* tile_sum, uint32_t* order, uint32_t* scratch,
+                            hipStream_t stream);
 const char* hrt_last_kernel();
 void hrt_reset_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
@@ -181,11 +182,13 @@ struct rt_renderer {
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
-    // cost-ordered dealing (rt_params.cost_order): per-tile query counts of the last sample-buffer launch, the tile
-    // order built from them for the next one, the counting sort's histogram / cursors; cost_tiles: the tile count
-    // they were set up for, order_tiles: the tile count tile_order holds a permutation of (0: none yet)
-    DevBuf<uint32_t> tile_cost, tile_order, order_scratch;
+    // cost-ordered dealing (rt_params.cost_order): per-pixel query counts of a learning launch (zeroed again by the
+    // sort), per-tile sums, the tile order built from them, the counting sort's histogram / cursors; cost_tiles: the
+    // tile count they were set up for, order_tiles: the tile count tile_order holds a permutation of (0: none yet);
+    // cost_learn: the next sample-buffer launch learns (set by every scene, camera, size or parameter change)
+    DevBuf<uint32_t> tile_cost, tile_sum, tile_order, order_scratch;
     uint32_t cost_tiles = 0, order_tiles = 0;
+    bool cost_learn = true;
     uint32_t last_ordered = 0;  // trace launches of the last sample-queue draw that dealt in cost order
     DevBuf<unsigned long long> wave_trace;  // diagnostic build only
     size_t wave_trace_words = 0;
@@ -214,7 +217,8 @@ struct rt_renderer {
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
                tri_geo.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
-               wave_trace.bytes() + steal_slots.bytes() + tile_cost.bytes() + tile_order.bytes() + order_scratch.bytes();
+               wave_trace.bytes() + steal_slots.bytes() + tile_cost.bytes() + tile_sum.bytes() + tile_order.bytes() +
+               order_scratch.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
     size_t image_floats() const { return (size_t)local_rows() * width * 3u; }
@@ -692,22 +696,25 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         rc = ensure(r->steal_slots, P.steal_cap);
         if (rc) return rc;
         P.steal_slots = r->steal_slots.ptr;
-        // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): every sample-buffer launch sums its
-        // samples' queries per tile, and the next launch (of this draw or the next) deals the tiles most expensive
-        // first, so the jobs that take longest start first instead of trailing the launch. Bit-identical in any order.
+        // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): a learning launch counts its samples'
+        // queries per pixel and the tiles are sorted by their sums, most expensive first; the following launches (of
+        // this draw and the next ones) deal their tiles in that order, so the jobs that take longest start first
+        // instead of trailing the launch. The renderer learns in its first sample-buffer launch after any scene,
+        // camera, size or parameter change (cost_order 2: in every launch). Bit-identical in any order.
         const bool cost_on = !P.ring_mode && r->params.cost_order != 1u;
         if (cost_on && r->cost_tiles != ntiles) {
             constexpr size_t SCRATCH = 2u * 128u;  // 2 x ORDER_BUCKETS
-            rc = ensure(r->tile_cost, ntiles);
+            rc = ensure(r->tile_cost, (size_t)ntiles * 64u);
+            if (!rc) rc = ensure(r->tile_sum, ntiles);
             if (!rc) rc = ensure(r->tile_order, ntiles);
             if (!rc) rc = ensure(r->order_scratch, SCRATCH);
             if (rc) return rc;
-            HIP_TRY(hipMemsetAsync(r->tile_cost.ptr, 0, (size_t)ntiles * sizeof(uint32_t), r->stream));
+            HIP_TRY(hipMemsetAsync(r->tile_cost.ptr, 0, (size_t)ntiles * 64u * sizeof(uint32_t), r->stream));
             HIP_TRY(hipMemsetAsync(r->order_scratch.ptr, 0, SCRATCH * sizeof(uint32_t), r->stream));
             r->cost_tiles = ntiles;
             r->order_tiles = 0;
+            r->cost_learn = true;
         }
-        P.tile_cost = cost_on ? r->tile_cost.ptr : nullptr;
         P.queue = r->counter.ptr + 15u;
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
@@ -753,13 +760,17 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
             P.tile_order = cost_on && r->order_tiles == ntiles ? r->tile_order.ptr : nullptr;
             ordered += P.tile_order ? 1u : 0u;
+            const bool learn = cost_on && (r->cost_learn || r->params.cost_order == 2u);
+            P.tile_cost = learn ? r->tile_cost.ptr : nullptr;
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
             r->trace_pairs_pending++;
             launches++;
-            if (cost_on) {  // (three small kernels, not counted in rt_stats.launches)
-                HIP_TRY(hrt_launch_order(r->tile_cost.ptr, ntiles, r->tile_order.ptr, r->order_scratch.ptr, r->stream));
+            if (learn) {  // (three small kernels, not counted in rt_stats.launches)
+                HIP_TRY(hrt_launch_order(r->tile_cost.ptr, ntiles, r->tile_sum.ptr, r->tile_order.ptr, r->order_scratch.ptr,
+                                         r->stream));
                 r->order_tiles = ntiles;
+                r->cost_learn = false;
             }
             if (!P.ring_mode) {
                 HIP_TRY(hrt_launch_accumulate(P, r->stream));
@@ -883,6 +894,7 @@ void delete_buffers(rt_renderer* r) {
     r->ring_ctl.release();
     r->wave_trace.release();
     r->tile_cost.release();
+    r->tile_sum.release();
     r->tile_order.release();
     r->order_scratch.release();
     r->cost_tiles = r->order_tiles = 0;
@@ -1003,6 +1015,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
     r->params = *p;
+    r->cost_learn = true;
     if (rows_changed) {
         r->frame_count = 0;
         int rc = zero_image(r);
@@ -1016,6 +1029,7 @@ int rt_set_camera(rt_renderer* r, const void* camera80) {
     if (!r || !camera80) return fail(RT_ERR_ARG, "rt_set_camera: null");
     std::memcpy(&r->camera, camera80, sizeof(hrt::Camera));
     r->has_camera = true;
+    r->cost_learn = true;
     return RT_OK;
 }
 
@@ -1027,6 +1041,7 @@ int rt_set_spheres(rt_renderer* r, const void* spheres48, uint32_t n) {
     if (n >= (1u << 28)) return fail(RT_ERR_ARG, "rt_set_spheres: more than 2^28 spheres");
     r->spheres.resize(n);
     if (n) std::memcpy(r->spheres.data(), spheres48, (size_t)n * sizeof(hrt::Sphere));
+    r->cost_learn = true;
     return upload_spheres(r);
 }
 
@@ -1038,6 +1053,7 @@ int rt_set_bvh(rt_renderer* r, const uint32_t sizes[2], const void* nodes32, uin
     const uint32_t n = sizes[0], m = sizes[1];
     if (int rc = rt_host_check_bvh_sizes(sizes, n_nodes, n_tris, n_mats)) return rc;
     if ((n && !nodes32) || (m && !tris64) || (n_mats && !mats32)) return fail(RT_ERR_ARG, "rt_set_bvh: null buffer");
+    r->cost_learn = true;
     const hrt::Triangle* T = (const hrt::Triangle*)tris64;
     std::vector<hrt_dev::TriDev> td(m);
     for (uint32_t j = 0; j < m; j++) {
@@ -1200,6 +1216,7 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (ds.rc) return ds.rc;
     r->width = std::max<uint32_t>(1, width);  // renderer.rs:274-275
     r->height = std::max<uint32_t>(1, height);
+    r->cost_learn = true;
     r->frame_count = 0;
     return zero_image(r);
 }

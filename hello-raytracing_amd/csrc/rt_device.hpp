@@ -177,9 +177,9 @@ struct KParams {
     // the triangles' test operands alone, a | e1 | e2 as 9 floats (36 B) per triangle (the deferred tests of the
     // split kernels, tri_test<TBUF>): 35 KB for Suzanne instead of the 64-B records' 63 KB in the CU's 32-KB L1
     const float* tri_geo;
-    // cost-ordered dealing (sample buffer; rt_params.cost_order): every finished sample adds its query count to its
-    // tile's cost; the next launch deals the tiles in descending cost order (rt_kernels.hip k_order_*), null = off /
-    // the identity order
+    // cost-ordered dealing (sample buffer; rt_params.cost_order): in a learning launch every finished sample adds its
+    // query count to its pixel's counter (tile_cost[pix], null = not learning); tile_order (null = raster order): the
+    // tiles in descending order of their last learnt cost (rt_kernels.hip k_order_*)
     uint32_t* tile_cost;
     const uint32_t* tile_order;
 };

@@ -1474,7 +1474,9 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
         o[0] = c.x;
         o[1] = c.y;
         o[2] = c.z;
-        if (uint32_t* const tc = K->tile_cost) __hip_atomic_fetch_add(tc + (pix >> 6), cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (one counter per pixel: a wave's stores of one tile-frame add to 64 different words; one word per tile
+        // serialised the 64 atomics and cost C3 4x in the launches that counted)
+        if (uint32_t* const tc = K->tile_cost) __hip_atomic_fetch_add(tc + pix, cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     const uint32_t slot = J.w[WJ_SLOT + (ref >> 16)];  // per-lane entry: an LDS read, not a uniform value
@@ -2921,30 +2923,44 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Cost-ordered dealing (rt_params.cost_order; renderer.cpp): after a sample-buffer launch the tiles are ordered by the
-// queries their samples took in it (tile_cost, summed by ring_store), most expensive first, and the next launch deals
-// its jobs in that tile order (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths stay in
-// glass for the bounce cap costs ~25x a sky tile; dealt late, its jobs outlast the launch (C4's 1/8 share: queue
-// drained at 17 ms, last wave at 38 ms without stealing, 21.5 with it). The order is a counting sort on ORDER_BUCKETS
-// log-scale cost classes (4 per octave; order within a class is arbitrary): which wave traces a sample never changes
-// its colour or its place in the sample buffer, so the image is bit-identical in any order.
+// Cost-ordered dealing (rt_params.cost_order; renderer.cpp): a launch that learns sums its samples' queries per pixel
+// (pixel_cost, ring_store), and the tiles are then ordered by their sums, most expensive first; later launches deal
+// their jobs in that tile order (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths
+// bounce in crevices up to the bounce cap costs many times a sky tile; dealt late, its jobs outlast the launch (C4's
+// 1/8 share: queue drained at 17 ms, last wave at 38 ms without stealing, 21.5 with it). The order is a counting sort
+// on ORDER_BUCKETS log-scale cost classes (4 per octave; the order within a class is arbitrary): which wave traces a
+// sample never changes its colour or its place in the sample buffer, so the image is bit-identical in any order.
 constexpr uint32_t ORDER_BUCKETS = 128;
 __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
-    // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, < 2^32: < 128),
-    // most expensive first
+    // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, <= 2^32: the
+    // class of 2^32 is clamped), most expensive first
     const uint32_t k = (__float_as_uint((float)cost + 1.0f) >> 21) - (127u << 2);
     return (ORDER_BUCKETS - 1u) - min(k, ORDER_BUCKETS - 1u);
 }
-__global__ __launch_bounds__(256) void k_order_hist(const uint32_t* __restrict__ cost, uint32_t ntiles, uint32_t* hist) {
+// one wave per tile: the tile's 64 pixel counters summed (saturating) into tile_sum and zeroed for the next learning
+// launch, the tile's class counted in hist
+__global__ __launch_bounds__(256) void k_order_hist(uint32_t* __restrict__ pixel_cost, uint32_t ntiles,
+                                                    uint32_t* __restrict__ tile_sum, uint32_t* hist) {
     __shared__ uint32_t h[ORDER_BUCKETS];
     for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) h[b] = 0u;
     __syncthreads();
-    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < ntiles; t += gridDim.x * 256u) atomicAdd(&h[order_bucket(cost[t])], 1u);
+    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (t < ntiles) {  // (wave-uniform)
+        unsigned long long v = pixel_cost[(size_t)t * 64u + lane];
+        pixel_cost[(size_t)t * 64u + lane] = 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0u) {
+            const uint32_t c = (uint32_t)min(v, 0xFFFFFFFFull);
+            tile_sum[t] = c;
+            atomicAdd(&h[order_bucket(c)], 1u);
+        }
+    }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u)
         if (h[b]) atomicAdd(hist + b, h[b]);
 }
-// one workgroup: hist -> exclusive prefix sums (the classes' first positions) in cursor, hist zeroed for the next launch
+// one workgroup: hist -> exclusive prefix sums (the classes' first positions) in cursor, hist zeroed for the next sort
 __global__ __launch_bounds__(ORDER_BUCKETS) void k_order_scan(uint32_t* hist, uint32_t* cursor) {
     __shared__ uint32_t v[ORDER_BUCKETS];
     const uint32_t b = threadIdx.x;
@@ -2959,20 +2975,19 @@ __global__ __launch_bounds__(ORDER_BUCKETS) void k_order_scan(uint32_t* hist, ui
     }
     cursor[b] = b ? v[b - 1u] : 0u;
 }
-__global__ __launch_bounds__(256) void k_order_scatter(uint32_t* cost, uint32_t ntiles, uint32_t* cursor, uint32_t* order) {
+__global__ __launch_bounds__(256) void k_order_scatter(const uint32_t* __restrict__ tile_sum, uint32_t ntiles,
+                                                       uint32_t* cursor, uint32_t* __restrict__ order) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= ntiles) return;
-    const uint32_t pos = atomicAdd(cursor + order_bucket(cost[t]), 1u);
-    order[pos] = t;
-    cost[t] = 0u;  // the next launch's costs
+    order[atomicAdd(cursor + order_bucket(tile_sum[t]), 1u)] = t;
 }
 // scratch: 2 * ORDER_BUCKETS words, zero on the first call (k_order_scan leaves the histogram zeroed)
-hipError_t hrt_launch_order(uint32_t* cost, uint32_t ntiles, uint32_t* order, uint32_t* scratch, hipStream_t stream) {
+hipError_t hrt_launch_order(uint32_t* pixel_cost, uint32_t ntiles, uint32_t* tile_sum, uint32_t* order, uint32_t* scratch,
+                            hipStream_t stream) {
     if (ntiles == 0) return hipSuccess;
-    const unsigned blocks = (unsigned)std::min<uint32_t>((ntiles + 255u) / 256u, 1024u);
-    hipLaunchKernelGGL(k_order_hist, dim3(blocks), dim3(256), 0, stream, cost, ntiles, scratch);
+    hipLaunchKernelGGL(k_order_hist, dim3((ntiles + 3u) / 4u), dim3(256), 0, stream, pixel_cost, ntiles, tile_sum, scratch);
     hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_BUCKETS), 0, stream, scratch, scratch + ORDER_BUCKETS);
-    hipLaunchKernelGGL(k_order_scatter, dim3((ntiles + 255u) / 256u), dim3(256), 0, stream, cost, ntiles,
+    hipLaunchKernelGGL(k_order_scatter, dim3((ntiles + 255u) / 256u), dim3(256), 0, stream, tile_sum, ntiles,
                        scratch + ORDER_BUCKETS, order);
     return hipGetLastError();
 }

@@ -115,11 +115,12 @@ typedef struct rt_params {
                                   (rt_stats.box_tests / sphere_tests); 0 (default): the sphere program's
                                   k_trace_split does not count them (reported 0; 1.3 % of C3's kernel
                                   time); the other kernels always count                                  */
-    uint32_t cost_order;       /* sample queue with the sample buffer: deal each launch's tiles in descending
-                                  order of the queries their samples took in the renderer's previous launch
-                                  (of this draw or an earlier one with the same tile count), so the slowest
-                                  jobs start first; the first launch deals in raster order. 0 auto = on,
-                                  1 off, 2 on; bit-identical always               */
+    uint32_t cost_order;       /* sample queue with the sample buffer: deal a launch's tiles in descending order
+                                  of the queries their samples took in a learning launch, so the slowest jobs
+                                  start first. 0 auto: the first sample-buffer launch after a change of scene,
+                                  camera, size or parameters learns (dealing in the last order learnt, or in
+                                  raster order), the later ones deal in its order; 1 off (raster order);
+                                  2 every launch learns for the next; bit-identical always */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u
