@@ -269,11 +269,15 @@ __device__ __forceinline__ int bvh_slot_of(const KParams& P, int code) {
     return (uint32_t)code < P.bvh_nleaf ? P.bvh_slot[code] : P.large_slots[code - (int)P.bvh_nleaf];
 }
 
+template <bool H16, bool SO>
+__device__ __forceinline__ void bvh_slab(const KParams& P, const Ray& r, BvhQuery& Q);
+
 // Returns true when the walk has to run (false: bvh_end does the full scan).
 // SO (k_trace_split's sign-ordered box test, box_hit_so): Q.S.lo / hi hold the near / far plane constants instead of
 // the min / max ones (swapped per axis where 1/d < 0).
 // COUNT false (k_trace_split without rt_params.count_tests): no box / sphere test counts (1.3 % of C3's kernel time).
-template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false, bool COUNT = true>
+// SLAB false: the slab constants and the root are left to the caller (the mixed kernel's suspendable sphere walk)
+template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false, bool COUNT = true, bool SLAB = true>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -298,7 +302,18 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     if constexpr (COUNT) tally.spheres += nlarge;
     Q.bt = bt;
     Q.bc = bc;
+    if constexpr (SLAB) {
+        bvh_slab<H16, SO>(P, r, Q);
+        Q.node = P.bvh_root;
+    }
+    return true;
+}
 
+// The walk's slab constants (bvh_begin; recomputed from the ray when a suspended sphere walk of the mixed kernel
+// resumes: the same operations, the same bits)
+template <bool H16, bool SO>
+__device__ __forceinline__ void bvh_slab(const KParams& P, const Ray& r, BvhQuery& Q) {
+    const float a = dot(r.d, r.d);
     // per-query padding: delta >= the distance by which a float-accepted sphere can miss geometrically
     const f3 op = mk(r.o.x - P.bvh_rc[0], r.o.y - P.bvh_rc[1], r.o.z - P.bvh_rc[2]);
     const float dl = __builtin_amdgcn_sqrtf(dot(op, op));
@@ -320,8 +335,6 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     }
     Q.S.lo = Q.S.lo * Q.S.inv;
     Q.S.hi = Q.S.hi * Q.S.inv;
-    Q.node = P.bvh_root;
-    return true;
 }
 
 // The walk. Returns true when it has finished; with SUSPEND it may return false after a pop, once fewer
@@ -2724,6 +2737,9 @@ constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
 constexpr uint32_t heap_list_words(int hl, int scan) { return hl == 0 ? TRI_BATCH : (hl == 3 && scan != SCAN_BVH) ? 7u : 8u; }
 constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : 1024u; }
 
+#ifndef HRT_SPHERE_SUSPEND
+#define HRT_SPHERE_SUSPEND 1
+#endif
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
@@ -2770,9 +2786,11 @@ k_trace_split_tris(const KParams P) {
     float sky_t = 0.0f;
     uint32_t s = 0, bounce = 0, pix = 0, fl = 0;
     bool have = false;
-    // query state: 0 start, 3 heap walk, 4 shade, 5 sky only
+    // query state: 0 start, 1 sphere walk suspended (SPHERE_SUSPEND), 3 heap walk, 4 shade, 5 sky only
     uint32_t qs = 0;
-    int bi = -1;  // sphere winner slot
+    // the culling-BVH sphere walk suspendable like the heap walk (the HL3 kernel's no-overflow walk; round 5)
+    constexpr bool SPHERE_SUSPEND = HRT_SPHERE_SUSPEND && MODE == MODE_MIXED && SCAN == SCAN_BVH && HL > 0;
+    // the sphere winner rides in the heap walk's winner code: W.bj = -2 - slot until a triangle beats it (-1: no hit)
     HeapWalk W;
     HRT_PHASE_DECL;
 #ifdef HRT_STAMPS
@@ -2796,18 +2814,60 @@ k_trace_split_tris(const KParams P) {
             if (bounce >= P.bounces) {
                 qs = 5u;  // bounce cap 0: the sample is the sky colour
             } else if constexpr (MODE == MODE_TRIS) {
-                bi = -1;
                 heap_begin(ray, FLT_MAX_REF, W);
                 qs = 3u;
+            } else if constexpr (SPHERE_SUSPEND) {
+                // the sphere walk's state (node, stack depth, winner t and code) lives in the heap walk's registers
+                // until its heap walk begins: W.i, W.step, W.best, W.bj
+                float sb = FLT_MAX_REF;
+                BvhQuery Q;
+                if (bvh_begin<true, false, true, true, true, false>(P, ray, sb, Q, tally)) {
+                    W.i = P.bvh_root;
+                    W.step = 0u;
+                    W.best = Q.bt;
+                    W.bj = Q.bc;
+                    qs = 1u;
+                } else {  // (uncovered ray: the exact full scan)
+                    const int bi = bvh_end<true>(P, ray, Q, sb, tally);
+                    heap_begin<false>(ray, sb, W);
+                    W.bj = -2 - bi;
+                    qs = 3u;
+                }
             } else {
                 float sb = FLT_MAX_REF;
+                int bi;
                 // (HL > 0: renderer.cpp runs these only for sphere trees of depth <= 8 = SPHERE_STACK: no overflow)
                 if constexpr (SCAN == SCAN_BVH) bi = scan_spheres_bvh<SPHERE_STACK, true, WGT, true, (HL > 0), true>(P, ray, sb, sstack, tally);
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
                 heap_begin<SCAN != SCAN_BVH>(ray, sb, W);
+                W.bj = -2 - bi;
                 qs = 3u;
+            }
+        }
+        if (SPHERE_SUSPEND && have && qs == 1u) {
+            // New and suspended sphere walks step together (the slab constants computed from the ray, the stack in the
+            // lane's list words), and the walk is left once fewer than suspend_below lanes still walk: the half of its
+            // wave steps that ran with ~5 lanes when it ran to completion (C5, scripts/diag_tris.py) is not waited for
+            BvhQuery Q;
+            Q.full_scan = 0u;
+            Q.node = W.i;
+            Q.sp = (int)W.step;
+            Q.bt = W.best;
+            Q.bc = W.bj;
+            bvh_slab<true, true>(P, ray, Q);
+            if (bvh_run<true, SPHERE_STACK, false, true, WGT, true, true>(P, ray, Q, sstack, tally, suspend_below, P.bvh_hnodes)) {
+                float sb;
+                const int bi = bvh_end<true>(P, ray, Q, sb, tally);
+                heap_begin<false>(ray, sb, W);
+                W.bj = -2 - bi;
+                qs = 3u;
+            } else {
+                W.i = Q.node;
+                W.step = (uint32_t)Q.sp;
+                W.best = Q.bt;
+                W.bj = Q.bc;
             }
         }
         HRT_PHASE(1);
@@ -2842,7 +2902,7 @@ k_trace_split_tris(const KParams P) {
                 Hit h;
                 bool hit = true;
                 if (W.bj >= 0) tri_record(P, ray, P.tris[W.bj], W.best, h);
-                else if (bi >= 0) sphere_record(P, ray, bi, W.best, h);
+                else if (W.bj <= -2) sphere_record(P, ray, -2 - W.bj, W.best, h);
                 else hit = false;
                 if (hit) {
                     scatter<MODE>(P, s, ray, h);
