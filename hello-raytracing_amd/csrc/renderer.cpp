@@ -27,6 +27,7 @@ hipError_t hrt_launch_accumulate(const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_trace(int mode, int variant, const hrt_dev::KParams& P, hipStream_t stream);
 hipError_t hrt_launch_order(uint32_t* pixel_cost, uint32_t ntiles, uint32_t* tile_sum, uint32_t* order, uint32_t* scratch,
                             hipStream_t stream);
+uint32_t hrt_order_scratch_words(uint32_t ntiles);
 const char* hrt_last_kernel();
 void hrt_reset_last_kernel();
 hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned long long* out_dev, hipStream_t st);
@@ -703,7 +704,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // camera, size or parameter change (cost_order 2: in every launch). Bit-identical in any order.
         const bool cost_on = !P.ring_mode && r->params.cost_order != 1u;
         if (cost_on && r->cost_tiles != ntiles) {
-            constexpr size_t SCRATCH = 2u * 128u;  // 2 x ORDER_BUCKETS
+            const size_t SCRATCH = hrt_order_scratch_words(ntiles);
             rc = ensure(r->tile_cost, (size_t)ntiles * 64u);
             if (!rc) rc = ensure(r->tile_sum, ntiles);
             if (!rc) rc = ensure(r->tile_order, ntiles);

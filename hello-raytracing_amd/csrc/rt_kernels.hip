@@ -276,8 +276,7 @@ __device__ __forceinline__ void bvh_slab(const KParams& P, const Ray& r, BvhQuer
 // SO (k_trace_split's sign-ordered box test, box_hit_so): Q.S.lo / hi hold the near / far plane constants instead of
 // the min / max ones (swapped per axis where 1/d < 0).
 // COUNT false (k_trace_split without rt_params.count_tests): no box / sphere test counts (1.3 % of C3's kernel time).
-// SLAB false: the slab constants and the root are left to the caller (the mixed kernel's suspendable sphere walk)
-template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false, bool COUNT = true, bool SLAB = true>
+template <bool H16 = false, bool FAST = false, bool KA = false, bool SO = false, bool COUNT = true>
 __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float best, BvhQuery& Q, Tally& tally) {
     const float a = dot(r.d, r.d);
     const float a4 = 4.0f * a, a2 = 2.0f * a;  // recomputed by bvh_run: fewer registers live across rounds
@@ -302,15 +301,12 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     if constexpr (COUNT) tally.spheres += nlarge;
     Q.bt = bt;
     Q.bc = bc;
-    if constexpr (SLAB) {
-        bvh_slab<H16, SO>(P, r, Q);
-        Q.node = P.bvh_root;
-    }
+    bvh_slab<H16, SO>(P, r, Q);
+    Q.node = P.bvh_root;
     return true;
 }
 
-// The walk's slab constants (bvh_begin; recomputed from the ray when a suspended sphere walk of the mixed kernel
-// resumes: the same operations, the same bits)
+// The walk's slab constants (bvh_begin)
 template <bool H16, bool SO>
 __device__ __forceinline__ void bvh_slab(const KParams& P, const Ray& r, BvhQuery& Q) {
     const float a = dot(r.d, r.d);
@@ -2737,9 +2733,6 @@ constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
 constexpr uint32_t heap_list_words(int hl, int scan) { return hl == 0 ? TRI_BATCH : (hl == 3 && scan != SCAN_BVH) ? 7u : 8u; }
 constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : 1024u; }
 
-#ifndef HRT_SPHERE_SUSPEND
-#define HRT_SPHERE_SUSPEND 1
-#endif
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
@@ -2786,10 +2779,8 @@ k_trace_split_tris(const KParams P) {
     float sky_t = 0.0f;
     uint32_t s = 0, bounce = 0, pix = 0, fl = 0;
     bool have = false;
-    // query state: 0 start, 1 sphere walk suspended (SPHERE_SUSPEND), 3 heap walk, 4 shade, 5 sky only
+    // query state: 0 start, 3 heap walk, 4 shade, 5 sky only
     uint32_t qs = 0;
-    // the culling-BVH sphere walk suspendable like the heap walk (the HL3 kernel's no-overflow walk; round 5)
-    constexpr bool SPHERE_SUSPEND = HRT_SPHERE_SUSPEND && MODE == MODE_MIXED && SCAN == SCAN_BVH && HL > 0;
     // the sphere winner rides in the heap walk's winner code: W.bj = -2 - slot until a triangle beats it (-1: no hit)
     HeapWalk W;
     HRT_PHASE_DECL;
@@ -2816,23 +2807,6 @@ k_trace_split_tris(const KParams P) {
             } else if constexpr (MODE == MODE_TRIS) {
                 heap_begin(ray, FLT_MAX_REF, W);
                 qs = 3u;
-            } else if constexpr (SPHERE_SUSPEND) {
-                // the sphere walk's state (node, stack depth, winner t and code) lives in the heap walk's registers
-                // until its heap walk begins: W.i, W.step, W.best, W.bj
-                float sb = FLT_MAX_REF;
-                BvhQuery Q;
-                if (bvh_begin<true, false, true, true, true, false>(P, ray, sb, Q, tally)) {
-                    W.i = P.bvh_root;
-                    W.step = 0u;
-                    W.best = Q.bt;
-                    W.bj = Q.bc;
-                    qs = 1u;
-                } else {  // (uncovered ray: the exact full scan)
-                    const int bi = bvh_end<true>(P, ray, Q, sb, tally);
-                    heap_begin<false>(ray, sb, W);
-                    W.bj = -2 - bi;
-                    qs = 3u;
-                }
             } else {
                 float sb = FLT_MAX_REF;
                 int bi;
@@ -2844,30 +2818,6 @@ k_trace_split_tris(const KParams P) {
                 heap_begin<SCAN != SCAN_BVH>(ray, sb, W);
                 W.bj = -2 - bi;
                 qs = 3u;
-            }
-        }
-        if (SPHERE_SUSPEND && have && qs == 1u) {
-            // New and suspended sphere walks step together (the slab constants computed from the ray, the stack in the
-            // lane's list words), and the walk is left once fewer than suspend_below lanes still walk: the half of its
-            // wave steps that ran with ~5 lanes when it ran to completion (C5, scripts/diag_tris.py) is not waited for
-            BvhQuery Q;
-            Q.full_scan = 0u;
-            Q.node = W.i;
-            Q.sp = (int)W.step;
-            Q.bt = W.best;
-            Q.bc = W.bj;
-            bvh_slab<true, true>(P, ray, Q);
-            if (bvh_run<true, SPHERE_STACK, false, true, WGT, true, true>(P, ray, Q, sstack, tally, suspend_below, P.bvh_hnodes)) {
-                float sb;
-                const int bi = bvh_end<true>(P, ray, Q, sb, tally);
-                heap_begin<false>(ray, sb, W);
-                W.bj = -2 - bi;
-                qs = 3u;
-            } else {
-                W.i = Q.node;
-                W.step = (uint32_t)Q.sp;
-                W.best = Q.bt;
-                W.bj = Q.bc;
             }
         }
         HRT_PHASE(1);
@@ -2983,24 +2933,29 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Cost-ordered dealing (rt_params.cost_order; renderer.cpp): a launch that learns sums its samples' queries per pixel
-// (pixel_cost, ring_store), and the tiles are then ordered by their sums, most expensive first; later launches deal
-// their jobs in that tile order (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths
-// bounce in crevices up to the bounce cap costs many times a sky tile; dealt late, its jobs outlast the launch (C4's
-// 1/8 share: queue drained at 17 ms, last wave at 38 ms without stealing, 21.5 with it). The order is a counting sort
-// on ORDER_BUCKETS log-scale cost classes (4 per octave; the order within a class is arbitrary): which wave traces a
-// sample never changes its colour or its place in the sample buffer, so the image is bit-identical in any order.
-constexpr uint32_t ORDER_BUCKETS = 128;
+// Cost-ordered dealing (rt_params.cost_order; renderer.cpp): a learning launch sums its samples' queries per pixel
+// (pixel_cost, ring_store); the tiles are then split into a head — the most expensive ones, at most ORDER_HEAD_PCT % of
+// them, by log-scale cost classes — and the rest, each in raster order, and later launches deal the head first
+// (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths bounce up to the cap costs many
+// times a sky tile; dealt late, its jobs outlast the launch. A full sort by cost measured slower: the GPU then works on
+// tiles from all over the image at once (C4 -2.3 %, C2 -5 %, C3 -0.8 % on full images: the rays of a band of adjacent
+// tiles share their scene data in the caches), and the head keeps raster order among the expensive tiles, which
+// cluster on the same objects. Which wave traces a sample never changes its colour or its place in the sample buffer,
+// so the image is bit-identical in any order.
+constexpr uint32_t ORDER_BUCKETS = 128, ORDER_HEAD_PCT = 25, ORDER_BLOCK = 1024;
 __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
     // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, <= 2^32: the
     // class of 2^32 is clamped), most expensive first
     const uint32_t k = (__float_as_uint((float)cost + 1.0f) >> 21) - (127u << 2);
     return (ORDER_BUCKETS - 1u) - min(k, ORDER_BUCKETS - 1u);
 }
+// scratch words: [0, 128) class histogram (zero between sorts), [128] the head's classes (class < cut), [129] head
+// size, [256, 256 + blocks) head tiles per ORDER_BLOCK tiles, then their exclusive prefix sums
+constexpr uint32_t OS_HIST = 0, OS_CUT = ORDER_BUCKETS, OS_NHEAD = ORDER_BUCKETS + 1, OS_BLK = 2 * ORDER_BUCKETS;
 // one wave per tile: the tile's 64 pixel counters summed (saturating) into tile_sum and zeroed for the next learning
-// launch, the tile's class counted in hist
+// launch, the tile's class counted
 __global__ __launch_bounds__(256) void k_order_hist(uint32_t* __restrict__ pixel_cost, uint32_t ntiles,
-                                                    uint32_t* __restrict__ tile_sum, uint32_t* hist) {
+                                                    uint32_t* __restrict__ tile_sum, uint32_t* scratch) {
     __shared__ uint32_t h[ORDER_BUCKETS];
     for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) h[b] = 0u;
     __syncthreads();
@@ -3018,39 +2973,100 @@ __global__ __launch_bounds__(256) void k_order_hist(uint32_t* __restrict__ pixel
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u)
-        if (h[b]) atomicAdd(hist + b, h[b]);
+        if (h[b]) atomicAdd(scratch + OS_HIST + b, h[b]);
 }
-// one workgroup: hist -> exclusive prefix sums (the classes' first positions) in cursor, hist zeroed for the next sort
-__global__ __launch_bounds__(ORDER_BUCKETS) void k_order_scan(uint32_t* hist, uint32_t* cursor) {
-    __shared__ uint32_t v[ORDER_BUCKETS];
-    const uint32_t b = threadIdx.x;
-    v[b] = hist[b];
-    hist[b] = 0u;
+// one thread: the head = the most expensive classes holding at most ORDER_HEAD_PCT % of the tiles (the histogram
+// zeroed for the next sort)
+__global__ void k_order_cut(uint32_t* scratch, uint32_t ntiles) {
+    if (threadIdx.x != 0u) return;
+    const uint32_t cap = (uint32_t)((unsigned long long)ntiles * ORDER_HEAD_PCT / 100u);
+    uint32_t n = 0, cut = 0;
+    bool open = true;
+    for (uint32_t b = 0; b < ORDER_BUCKETS; b++) {
+        const uint32_t c = scratch[OS_HIST + b];
+        scratch[OS_HIST + b] = 0u;
+        if (open && n + c <= cap) {
+            n += c;
+            cut = b + 1u;
+        } else {
+            open = false;
+        }
+    }
+    scratch[OS_CUT] = cut;
+    scratch[OS_NHEAD] = n;
+}
+__device__ __forceinline__ bool order_head(const uint32_t* tile_sum, const uint32_t* scratch, uint32_t t) {
+    return order_bucket(tile_sum[t]) < scratch[OS_CUT];
+}
+// head tiles per block of ORDER_BLOCK tiles (256 threads x 4 tiles)
+__global__ __launch_bounds__(256) void k_order_count(const uint32_t* __restrict__ tile_sum, uint32_t ntiles, uint32_t* scratch) {
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t t = blockIdx.x * ORDER_BLOCK + k * 256u + threadIdx.x;
+        c += t < ntiles && order_head(tile_sum, scratch, t) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    __shared__ uint32_t w[4];
+    if ((threadIdx.x & 63u) == 0u) w[threadIdx.x >> 6] = c;
     __syncthreads();
-    for (uint32_t o = 1; o < ORDER_BUCKETS; o <<= 1) {
-        const uint32_t add = b >= o ? v[b - o] : 0u;
+    if (threadIdx.x == 0) scratch[OS_BLK + blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+// one workgroup: exclusive prefix sums of the blocks' head counts, in place (nblocks <= 2^15)
+__global__ __launch_bounds__(1024) void k_order_blockscan(uint32_t* scratch, uint32_t nblocks) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nblocks + 1023u) / 1024u, b0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; k++) s += scratch[OS_BLK + b0 + k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024u; o <<= 1) {
+        const uint32_t add = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
         __syncthreads();
-        v[b] += add;
+        part[threadIdx.x] += add;
         __syncthreads();
     }
-    cursor[b] = b ? v[b - 1u] : 0u;
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1u] : 0u;
+    for (uint32_t k = 0; k < per && b0 + k < nblocks; k++) {
+        const uint32_t c = scratch[OS_BLK + b0 + k];
+        scratch[OS_BLK + b0 + k] = run;
+        run += c;
+    }
 }
+// stable partition: head tiles to [0, nhead) and the others to [nhead, ntiles), each in tile order
 __global__ __launch_bounds__(256) void k_order_scatter(const uint32_t* __restrict__ tile_sum, uint32_t ntiles,
-                                                       uint32_t* cursor, uint32_t* __restrict__ order) {
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= ntiles) return;
-    order[atomicAdd(cursor + order_bucket(tile_sum[t]), 1u)] = t;
+                                                       const uint32_t* scratch, uint32_t* __restrict__ order) {
+    __shared__ uint32_t w[4];
+    const uint32_t nhead = scratch[OS_NHEAD];
+    uint32_t before = scratch[OS_BLK + blockIdx.x];  // head tiles before this block's current group of 256
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t t = blockIdx.x * ORDER_BLOCK + k * 256u + threadIdx.x;
+        const bool h = t < ntiles && order_head(tile_sum, scratch, t);
+        const unsigned long long m = __ballot(h);
+        if (lane == 0u) w[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t r = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        for (uint32_t q = 0; q < wv; q++) r += w[q];
+        if (t < ntiles) order[h ? r : nhead + (t - r)] = t;
+        before += w[0] + w[1] + w[2] + w[3];
+        __syncthreads();
+    }
 }
-// scratch: 2 * ORDER_BUCKETS words, zero on the first call (k_order_scan leaves the histogram zeroed)
+// scratch: hrt_order_scratch_words(ntiles) words, the histogram zero on the first call
 hipError_t hrt_launch_order(uint32_t* pixel_cost, uint32_t ntiles, uint32_t* tile_sum, uint32_t* order, uint32_t* scratch,
                             hipStream_t stream) {
     if (ntiles == 0) return hipSuccess;
+    const uint32_t nblocks = (ntiles + ORDER_BLOCK - 1u) / ORDER_BLOCK;
+    if (nblocks > 32768u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_order_hist, dim3((ntiles + 3u) / 4u), dim3(256), 0, stream, pixel_cost, ntiles, tile_sum, scratch);
-    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_BUCKETS), 0, stream, scratch, scratch + ORDER_BUCKETS);
-    hipLaunchKernelGGL(k_order_scatter, dim3((ntiles + 255u) / 256u), dim3(256), 0, stream, tile_sum, ntiles,
-                       scratch + ORDER_BUCKETS, order);
+    hipLaunchKernelGGL(k_order_cut, dim3(1), dim3(64), 0, stream, scratch, ntiles);
+    hipLaunchKernelGGL(k_order_count, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch);
+    hipLaunchKernelGGL(k_order_blockscan, dim3(1), dim3(1024), 0, stream, scratch, nblocks);
+    hipLaunchKernelGGL(k_order_scatter, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch, order);
     return hipGetLastError();
 }
+uint32_t hrt_order_scratch_words(uint32_t ntiles) { return OS_BLK + (ntiles + ORDER_BLOCK - 1u) / ORDER_BLOCK; }
 
 // Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE
 // operations (correctly rounded in this build): n random cases per test, counted mismatches in out[0..2]:
