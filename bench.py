@@ -483,7 +483,8 @@ def main() -> int:
                     help="sample queue: frame-block work stealing, 0 auto (short launches), 1 off, 2 on")
     ap.add_argument("--tail-split", type=int, default=None, help="sample queue: 0 auto (quarter jobs at the end), 1 off")
     ap.add_argument("--cost-order", type=int, default=None,
-                    help="sample queue: 0 auto = deal tiles by the previous launch's cost, most expensive first; 1 off")
+                    help="sample queue: 0 auto (the most expensive tiles first for a row partition's shares "
+                         "without stealing), 1 off, 2 on")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,

@@ -698,24 +698,14 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         if (rc) return rc;
         P.steal_slots = r->steal_slots.ptr;
         // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): a learning launch counts its samples'
-        // queries per pixel and the tiles are sorted by their sums, most expensive first; the following launches (of
-        // this draw and the next ones) deal their tiles in that order, so the jobs that take longest start first
-        // instead of trailing the launch. The renderer learns in its first sample-buffer launch after any scene,
-        // camera, size or parameter change (cost_order 2: in every launch). Bit-identical in any order.
-        const bool cost_on = !P.ring_mode && r->params.cost_order != 1u;
-        if (cost_on && r->cost_tiles != ntiles) {
-            const size_t SCRATCH = hrt_order_scratch_words(ntiles);
-            rc = ensure(r->tile_cost, (size_t)ntiles * 64u);
-            if (!rc) rc = ensure(r->tile_sum, ntiles);
-            if (!rc) rc = ensure(r->tile_order, ntiles);
-            if (!rc) rc = ensure(r->order_scratch, SCRATCH);
-            if (rc) return rc;
-            HIP_TRY(hipMemsetAsync(r->tile_cost.ptr, 0, (size_t)ntiles * 64u * sizeof(uint32_t), r->stream));
-            HIP_TRY(hipMemsetAsync(r->order_scratch.ptr, 0, SCRATCH * sizeof(uint32_t), r->stream));
-            r->cost_tiles = ntiles;
-            r->order_tiles = 0;
-            r->cost_learn = true;
-        }
+        // queries per pixel and the tiles are split into the most expensive quarter and the rest; the following launches
+        // (of this draw and the next ones) deal that head first, each part in raster order, so the jobs that take
+        // longest start early instead of trailing the launch. The renderer learns in its first ordered launch after any
+        // scene, camera, size or parameter change (cost_order 3: in every launch). Auto: a rank's share of a row
+        // partition (row_step > 1) without stealing — measured (profiles/r05/l/): 8-way splits C3 0.940 -> 0.960,
+        // C5 0.974 -> 0.987, C2 0.52 -> 0.59; full images C3 -0.2 %, C4 -0.6 %, C2 -2.3 %; with stealing (C4's
+        // shares) 0.757 -> 0.739. Bit-identical in any order.
+        const bool order_any = !P.ring_mode && r->params.cost_order != 1u;
         P.queue = r->counter.ptr + 15u;
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
@@ -759,9 +749,24 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             rc = trace_events(r, r->trace_pairs_pending);
             if (rc) return rc;
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
-            P.tile_order = cost_on && r->order_tiles == ntiles ? r->tile_order.ptr : nullptr;
+            const bool order_on =
+                order_any && (r->params.cost_order >= 2u || (r->params.row_step > 1u && !P.steal));
+            if (order_on && r->cost_tiles != ntiles) {
+                const size_t SCRATCH = hrt_order_scratch_words(ntiles);
+                rc = ensure(r->tile_cost, (size_t)ntiles * 64u);
+                if (!rc) rc = ensure(r->tile_sum, ntiles);
+                if (!rc) rc = ensure(r->tile_order, ntiles);
+                if (!rc) rc = ensure(r->order_scratch, SCRATCH);
+                if (rc) return rc;
+                HIP_TRY(hipMemsetAsync(r->tile_cost.ptr, 0, (size_t)ntiles * 64u * sizeof(uint32_t), r->stream));
+                HIP_TRY(hipMemsetAsync(r->order_scratch.ptr, 0, SCRATCH * sizeof(uint32_t), r->stream));
+                r->cost_tiles = ntiles;
+                r->order_tiles = 0;
+                r->cost_learn = true;
+            }
+            P.tile_order = order_on && r->order_tiles == ntiles ? r->tile_order.ptr : nullptr;
             ordered += P.tile_order ? 1u : 0u;
-            const bool learn = cost_on && (r->cost_learn || r->params.cost_order == 2u);
+            const bool learn = order_on && (r->cost_learn || r->params.cost_order == 3u);
             P.tile_cost = learn ? r->tile_cost.ptr : nullptr;
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
@@ -1011,7 +1016,8 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
     if (p->count_tests > 1) return fail(RT_ERR_ARG, "rt_set_params: count_tests must be 0 or 1");
-    if (p->cost_order > 2) return fail(RT_ERR_ARG, "rt_set_params: cost_order must be 0 auto, 1 off or 2 on");
+    if (p->cost_order > 3)
+        return fail(RT_ERR_ARG, "rt_set_params: cost_order must be 0 auto, 1 off, 2 on or 3 on, learning in every launch");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;

@@ -1899,6 +1899,10 @@ struct BlockQueue {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
     f3 pr_o = {0.0f, 0.0f, 0.0f}, pr_d = {0.0f, 0.0f, 0.0f};
     uint32_t pr_s = 0, pr_ok = 0;  // this lane's pixel's primary ray for the block, and whether it exists
+#ifdef HRT_STAMPS
+    uint32_t njobs = 0;                // (diagnostic build: jobs this wave took, and when it took its last one)
+    unsigned long long last_job = 0;
+#endif
 };
 
 // Free lanes (!have) take the next samples; sets drained once the job queue is empty.
@@ -1916,6 +1920,10 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             } else {
                 if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
+#ifdef HRT_STAMPS
+                B.njobs++;
+                B.last_job = hrt_realtime();
+#endif
             }
             B.blk_next = 0;
             const uint32_t x = (B.job_tile % P.tiles_w) * 8u + (lane & 7u);
@@ -2129,7 +2137,9 @@ struct WaveRecord {
     __device__ void drain(bool d) {
         if (d && drained == 0ull) drained = hrt_realtime() - start;
     }
-    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks) {
+    // last_job (k_trace): when the wave took its last job (s_memrealtime; 0: not recorded), as ticks from its start in
+    // bits 40-63 of word 2
+    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks, unsigned long long last_job = 0) {
         if (lane != 0u || P.wave_trace == nullptr) return;
         const unsigned long long end = hrt_realtime();
         unsigned hw, xcc;
@@ -2139,7 +2149,8 @@ struct WaveRecord {
         unsigned long long* rec = P.wave_trace + 4u * wid;
         rec[0] = start;
         rec[1] = end;
-        rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        const unsigned long long lj = last_job ? min(last_job - start, 0xFFFFFFull) : 0ull;
+        rec[2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) | (lj << 40);
         rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
     }
 };
@@ -2281,7 +2292,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
-    wrec.finish(P, lane, 0u);
+    wrec.finish(P, lane, BQ.njobs, BQ.last_job);
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)

@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# Round-5 batch M: the GPU suite with cost order auto (a row partition's shares without stealing), then same-box
+# A/Bs of --cost-order 1 against the default on C3 / C2 / C5 (8-way emulated splits; full images are unordered in both),
+# and the diagnostic build's wave records of 1/8 C2 shares with jobs per wave and the last job's time (k_trace).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+tag="${1:-r05m}"
+mkdir -p "gpurun_out/$tag"
+bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \
+  tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread || exit 1
+grep -q " passed" "gpurun_out/$tag/tests.log" && ! grep -q -E "[0-9]+ failed" "gpurun_out/$tag/tests.log" || exit 1
+for cfg in c3 c2; do
+  for round in 1 2; do
+    for co in 1 0; do
+      timeout -k 10 400 python bench.py --config $cfg --steps 3 --no-cpu-baseline --no-golden --cost-order $co \
+        > "gpurun_out/$tag/${cfg}_co$co.log" 2>&1 || exit 1
+      tail -1 "gpurun_out/$tag/${cfg}_co$co.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); e=d.get('emulated_split') or {}; print('$cfg cost_order $co', d['value'], d['ms_per_step'], e.get('efficiency'), e.get('predicted_ms_per_step'), [r['ms_per_step'] for r in e.get('per_rank', [])])"
+    done
+  done
+done | tee "gpurun_out/$tag/ab_cost_order.txt"
+HRT_LIB=lib/libhrt_diag.so bash scripts/gpu_step.sh "$tag/wave_tail_c2" 300 python scripts/wave_tail.py --config c2 --ranks 8 --rank 4 0 --full

@@ -34,6 +34,7 @@ def summarise(tr: np.ndarray) -> dict:
     st, en, info = st[ok], en[ok], tr[ok, 3].astype(np.int64)
     drained = info & 0xFFFFFFFF
     blocks = info >> 32
+    last_job = (tr[ok, 2].astype(np.uint64) >> np.uint64(40)).astype(np.int64)  # k_trace: when the last job was taken
     t0 = st.min()
     span = (en.max() - t0) / 1e5
     pct = lambda a: [round(float(np.percentile(a, q)), 3) for q in (0, 10, 50, 90, 100)]  # noqa: E731
@@ -49,7 +50,9 @@ def summarise(tr: np.ndarray) -> dict:
         "drain_ms_pcts": pct((st + drained - t0) / 1e5),
         "end_ms_pcts": pct((en - t0) / 1e5),
         "tail_after_first_drain_ms": round(float((en.max() - (st + drained).min()) / 1e5), 3),
-        "blocks_per_wave_pcts": pct(blocks),
+        "blocks_per_wave_pcts": pct(blocks),  # (k_trace: jobs per wave)
+        "last_job_ms_pcts": pct((st + last_job - t0) / 1e5) if last_job.any() else None,
+        "last_job_to_end_ms_pcts": pct((en - st - last_job) / 1e5) if last_job.any() else None,
         "blocks_total": int(blocks.sum()),
         "resident_waves_timeline": conc,
     }

@@ -661,19 +661,21 @@ def test_work_stealing_bit_identical(jf):
             assert runs[0][1][0] == q
 
 
-@pytest.mark.parametrize("steal,co", [(1, 2), (2, 2), (1, 0)])
+@pytest.mark.parametrize("steal,co", [(1, 3), (2, 3), (1, 2), (1, 0), (2, 0)])
 def test_cost_order_bit_identical(steal, co):
-    """Cost-ordered dealing (rt_params.cost_order; default 0 = learn once, 2 = learn in every launch): a launch deals
-    its tiles by a learning launch's per-tile query counts, most expensive first. A renderer's first draw deals its
-    first launch in raster order and the later launches in cost order, its second draw every launch in cost order;
-    both give the images and ray / node / triangle counts of raster-order draws (cost_order 1) and of the oracle —
-    sphere program (k_trace_split), mixed program (k_trace_split_tris, with the culling-BVH sphere walk too), the
-    linear scan (k_trace), with stealing on or off, tail parts, several launches per draw and a row block."""
+    """Cost-ordered dealing (rt_params.cost_order: 2 on, learning once; 3 on, learning in every launch; 0 auto = on for
+    a row partition's share without stealing): a launch deals the most expensive quarter of its tiles first (learnt from
+    a launch's per-pixel query counts), then the rest. A renderer's first draw deals its first launch in raster order
+    and the later launches in cost order, its second draw every launch in cost order; both give the images and ray /
+    node / triangle counts of raster-order draws (cost_order 1) and of the oracle — sphere program (k_trace_split),
+    mixed program (k_trace_split_tris, with the culling-BVH sphere walk too), the linear scan (k_trace), with stealing
+    on or off, tail parts, several launches per draw and a row block."""
     budget = lambda sd: max(1, (sd.width + 7) // 8 * ((sd.height + 7) // 8) * 64 * 12 * 7 >> 20)  # noqa: E731
     cases = [(scenes.config_c3(136, 80, 21), {}), (scenes.config_c4(120, 72, 16), {}),
              (scenes.config_c5(128, 72, 16), {}), (scenes.config_c2(96, 64, 16), {"variant": 1}),
              (scenes.config_c3(136, 80, 14), {"row0": 8, "row_step": 2, "row_block": 8}),
-             (scenes.config_c4(120, 72, 32), {"job_frames": 8, "tail_split": 2})]
+             (scenes.config_c4(120, 72, 32), {"job_frames": 8, "tail_split": 2}),
+             (scenes.config_c2(96, 64, 16), {"variant": 1, "row0": 0, "row_step": 3, "row_block": 8})]
     for sd, extra in cases:
         base = dict(schedule=hrt.RT_SCHEDULE_QUEUE, fold=hrt.RT_FOLD_BUFFER, steal=steal, **extra)
         r0 = scenes.make_renderer(sd)
@@ -685,15 +687,17 @@ def test_cost_order_bit_identical(steal, co):
         r = scenes.make_renderer(sd)
         # small colour budget: launches of ~7 frames, so the first draw already has ordered launches
         r.set_params(cost_order=co, queue_budget_mb=budget(sd) if sd.frames > 16 else 0, **base)
+        on = co >= 2 or (extra.get("row_step", 1) > 1 and (steal == 1 or sd.mode == hrt.RT_MODE_SPHERE and extra.get("variant") == 1))
         for k in range(2):
             r.reset_frame_count()
             r.draw_frames(sd.frames, 1000, 10)
             st = r.stats()
-            assert st.ordered_launches == st.trace_launches - (1 if k == 0 else 0), (sd.name, k, st.ordered_launches)
+            want_ordered = (st.trace_launches - (1 if k == 0 else 0)) if on else 0
+            assert st.ordered_launches == want_ordered, (sd.name, extra, k, st.ordered_launches, st.trace_launches)
             got = (r.read_image(), (st.queries, st.node_tests, st.tri_tests, st.sphere_tests, st.box_tests))
             np.testing.assert_array_equal(want[0].view(np.uint32), got[0].view(np.uint32), err_msg=f"{sd.name} draw {k}")
             assert want[1] == got[1], (sd.name, k, want[1], got[1])
-        if not extra and (steal, co) == (1, 2):
+        if not extra and (steal, co) == (1, 3):
             ref, q = scenes.oracle_render(sd)
             assert_parity(want[0], ref, f"{sd.name} cost order")
             assert want[1][0] == q
