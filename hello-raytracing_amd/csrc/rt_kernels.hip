@@ -2156,11 +2156,22 @@ struct WaveRecord {
 };
 #endif
 
-template <int MODE, int SCAN, bool TSAH = false>
-// 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
-// (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    TSAH || (MODE == MODE_MIXED && SCAN == SCAN_DEFER) ? 5 : 6))) void k_trace(const KParams P) {
+struct BlockState {
+    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
+#ifdef HRT_STAMPS
+    uint32_t nblocks = 0;  // (diagnostic build: frame blocks this wave generated, for its wave record)
+#endif
+};
+template <int MODE, bool STEAL, bool SEED>
+__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
+                                                 uint32_t* rows, uint32_t* okw, bool& drained,
+                                                 uint32_t lane, unsigned long long below, bool& have,
+                                                 uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
+                                                 uint32_t& bounce, uint32_t& pix, uint32_t& fl);
+
+// (the body of k_trace and k_trace_steal)
+template <int MODE, int SCAN, bool TSAH, bool STEAL>
+__device__ __forceinline__ void trace_queue(const KParams& P) {
     const uint32_t lane = threadIdx.x & 63u;
     const LaneLists lists = lane_lists<MODE, SCAN>();
     void* const lds_list = lists.sphere;
@@ -2173,6 +2184,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     // wave-uniform job state
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, job_next = 0, job_total = 0;
     BlockQueue BQ;  // frame-block refill (simple sphere scan only)
+    // STEAL (k_trace_steal): the frame block in LDS (refill_block_lds, as the split kernels: the stealing refill did not
+    // fit beside the block's registers)
+    __shared__ float blk_lds[STEAL ? 7 * 256 : 1];
+    __shared__ uint32_t blk_ok[STEAL ? 8 : 1];
+    BlockState BL;
+    uint32_t qs_unused = 0;
     __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     bool drained = false;
@@ -2200,7 +2217,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         constexpr bool BLOCK_REFILL = MODE == MODE_SPHERE && SCAN == SCAN_SIMPLE;
         bool need = !have && !drained;
         if constexpr (BLOCK_REFILL) {
-            refill_block<MODE>(P, BQ, J, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
+            if constexpr (STEAL)
+                refill_block_lds<MODE, true, true>(P, BL, J, blk_lds, nullptr, blk_ok, drained, lane, below, have, qs_unused,
+                                                   ray, att, sky_t, s, bounce, pix, fl);
+            else
+                refill_block<MODE>(P, BQ, J, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
             need = false;
         }
         unsigned long long m = __ballot(need);
@@ -2292,7 +2313,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
-    wrec.finish(P, lane, BQ.njobs, BQ.last_job);
+    if constexpr (STEAL) wrec.finish(P, lane, BL.nblocks);
+    else wrec.finish(P, lane, BQ.njobs, BQ.last_job);
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)
@@ -2332,6 +2354,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
+template <int MODE, int SCAN, bool TSAH = false>
+// 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
+// (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    TSAH || (MODE == MODE_MIXED && SCAN == SCAN_DEFER) ? 5 : 6))) void k_trace(const KParams P) {
+    trace_queue<MODE, SCAN, TSAH, false>(P);
+}
+// The linear sphere scan's frame-block refill with work stealing (rt_params.steal; short launches: a C2 job on the glass
+// sphere takes up to 1.7 ms, longer than a 1/8 share's whole launch)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_steal(const KParams P) {
+    trace_queue<MODE_SPHERE, SCAN_SIMPLE, false, true>(P);
+}
+
 // Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
 // compiles spill-free there): when the wave's block (one frame
 // of its job's 8x8 tile) is used up, every lane computes its own pixel's primary ray for the next frame at
@@ -2342,12 +2377,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // SEED (6 floats per lane) a taken sample's RNG state is recomputed from its pixel: it starts at (x * H + y) * time
 // (primary_ray) = the row's (x0 * H + y) * time + (x - x0) * H * time, per-row words in `rows` (9 per wave), then
 // five PCG steps. (Two float4 per lane before round 4: the bytes saved hold the whole heap top.)
-struct BlockState {
-    uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
-#ifdef HRT_STAMPS
-    uint32_t nblocks = 0;  // (diagnostic build: frame blocks this wave generated, for its wave record)
-#endif
-};
 
 
 template <int MODE, bool STEAL, bool SEED>
@@ -3233,6 +3262,12 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
     } else if constexpr (MODE == MODE_TRIS) {
         return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
     } else {
+        if constexpr (MODE == MODE_SPHERE && !TSAH) {  // (the frame-block refill: work stealing, rt_params.steal)
+            if (variant == SCAN_SIMPLE && P.steal) {
+                snprintf(g_kernel_name, sizeof g_kernel_name, "k_trace_steal");
+                return launch_persistent(k_trace_steal, P, stream, g_kernel_name);
+            }
+        }
         if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
         if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream, kname("k_trace", MODE, SCAN_DEFER, (int)TSAH));
         if constexpr (MODE == MODE_SPHERE) {
