@@ -726,9 +726,9 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 const bool fits = ntiles < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
                 const bool want = r->params.steal == 2u ||
                                   (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
-                // (the split kernels, and k_trace's frame-block refill for the linear sphere scan: k_trace_steal)
-                const bool can = split || (r->mode == RT_MODE_SPHERE && variant == hrt_dev::SCAN_SIMPLE);
-                P.steal = (can && !P.ring_mode && fits && want) ? 1u : 0u;
+                // (k_trace's frame-block refill for the linear sphere scan with the same stealing ran 3x slower, C2 80 ->
+                // 26 Grays/s: a claim per 64 cheap samples stalls the wave; profiles/r05/o/)
+                P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
             }
             // Tail split (the suspendable-walk kernels with the sample buffer, no stealing): the last ~2 jobs per
             // resident wave are dealt in parts (rt_params.tail_split: 2 quarters, 3 eighths; 0 auto = quarters),

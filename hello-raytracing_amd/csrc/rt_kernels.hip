@@ -1759,7 +1759,11 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
 #define HRT_CLAIM_FREE 32
 #endif
 constexpr uint32_t STEAL_OWN = HRT_STEAL_OWN;
-constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u;
+#ifndef HRT_STEAL_OWN_EARLY
+#define HRT_STEAL_OWN_EARLY 4
+#endif
+constexpr uint32_t STEAL_OWN_EARLY = HRT_STEAL_OWN_EARLY;
+constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u, ST_EARLY = 8u;
 // The tail (round 5): once the job queue is drained, a wave whose lanes are not all free claims another frame block only
 // when at least CLAIM_FREE of them are. A block claimed for a few free lanes waits for this wave's busy ones (paths of
 // up to 50 bounces) while other waves have run dry and exited: C4's 1/8 share drained its queue at 18.1 ms and ran to
@@ -1858,25 +1862,32 @@ __device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t la
     const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t st = J.get(WJ_ST);
     if (st & ST_OWN) {
-        if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)STEAL_OWN), STEAL_OWN);
+        const uint32_t own = st & ST_EARLY ? STEAL_OWN_EARLY : STEAL_OWN;
+        if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)own), own);
         if (claim_read(J, tile, frame)) return true;
-        J.set(WJ_ST, st & ~ST_OWN);
+        J.set(WJ_ST, st & ~(ST_OWN | ST_EARLY));
     }
     if (!(st & ST_QEMPTY)) {
+        uint32_t early = 0;
         if (lane == 0) {
             const uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
             unsigned long long v = 0;
-            if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
+            // a job dealt early (more than two jobs per wave still queued behind it) is claimed STEAL_OWN_EARLY frames
+            // at a time: no thief comes before the queue drains, and a claim per frame block stalls the wave
+            early = (unsigned long long)j + 2ull * K->nwaves < K->njobs ? 1u : 0u;
+            const uint32_t own = early ? STEAL_OWN_EARLY : STEAL_OWN;
+            if (j < K->njobs) {  // the new job's first `own` frames are ours with the exchange
                 const uint32_t tj = j / K->nchunks, c = j - tj * K->nchunks;
                 const uint32_t t = K->tile_order ? K->tile_order[tj] : tj;
                 const uint32_t nf = min(K->job_frames, K->nframes - c * K->job_frames);
                 v = ((unsigned long long)(t + 1u) << 39) | ((unsigned long long)c << 28) | ((unsigned long long)nf << 16);
-                (void)atomicExch(slots + wid, v + STEAL_OWN);
+                (void)atomicExch(slots + wid, v + own);
             }
-            claim_publish(J, K, v, STEAL_OWN);
+            claim_publish(J, K, v, own);
         }
+        early = uniform(__shfl(early, 0));
         if (claim_read(J, tile, frame)) {
-            J.set(WJ_ST, ST_OWN);
+            J.set(WJ_ST, ST_OWN | (early ? ST_EARLY : 0u));
             return true;
         }
     }
@@ -2162,16 +2173,11 @@ struct BlockState {
     uint32_t nblocks = 0;  // (diagnostic build: frame blocks this wave generated, for its wave record)
 #endif
 };
-template <int MODE, bool STEAL, bool SEED>
-__device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B, const WaveJobs& J, float* blk,
-                                                 uint32_t* rows, uint32_t* okw, bool& drained,
-                                                 uint32_t lane, unsigned long long below, bool& have,
-                                                 uint32_t& qs, Ray& ray, f3& att, float& sky_t, uint32_t& s,
-                                                 uint32_t& bounce, uint32_t& pix, uint32_t& fl);
-
-// (the body of k_trace and k_trace_steal)
-template <int MODE, int SCAN, bool TSAH, bool STEAL>
-__device__ __forceinline__ void trace_queue(const KParams& P) {
+template <int MODE, int SCAN, bool TSAH = false>
+// 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
+// (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    TSAH || (MODE == MODE_MIXED && SCAN == SCAN_DEFER) ? 5 : 6))) void k_trace(const KParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     const LaneLists lists = lane_lists<MODE, SCAN>();
     void* const lds_list = lists.sphere;
@@ -2184,12 +2190,6 @@ __device__ __forceinline__ void trace_queue(const KParams& P) {
     // wave-uniform job state
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, job_next = 0, job_total = 0;
     BlockQueue BQ;  // frame-block refill (simple sphere scan only)
-    // STEAL (k_trace_steal): the frame block in LDS (refill_block_lds, as the split kernels: the stealing refill did not
-    // fit beside the block's registers)
-    __shared__ float blk_lds[STEAL ? 7 * 256 : 1];
-    __shared__ uint32_t blk_ok[STEAL ? 8 : 1];
-    BlockState BL;
-    uint32_t qs_unused = 0;
     __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
     bool drained = false;
@@ -2217,11 +2217,7 @@ __device__ __forceinline__ void trace_queue(const KParams& P) {
         constexpr bool BLOCK_REFILL = MODE == MODE_SPHERE && SCAN == SCAN_SIMPLE;
         bool need = !have && !drained;
         if constexpr (BLOCK_REFILL) {
-            if constexpr (STEAL)
-                refill_block_lds<MODE, true, true>(P, BL, J, blk_lds, nullptr, blk_ok, drained, lane, below, have, qs_unused,
-                                                   ray, att, sky_t, s, bounce, pix, fl);
-            else
-                refill_block<MODE>(P, BQ, J, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
+            refill_block<MODE>(P, BQ, J, drained, lane, below, have, ray, att, sky_t, s, bounce, pix, fl);
             need = false;
         }
         unsigned long long m = __ballot(need);
@@ -2313,8 +2309,7 @@ __device__ __forceinline__ void trace_queue(const KParams& P) {
         job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
-    if constexpr (STEAL) wrec.finish(P, lane, BL.nblocks);
-    else wrec.finish(P, lane, BQ.njobs, BQ.last_job);
+    wrec.finish(P, lane, BQ.njobs, BQ.last_job);
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)
@@ -2354,18 +2349,6 @@ __device__ __forceinline__ void trace_queue(const KParams& P) {
     }
 }
 
-template <int MODE, int SCAN, bool TSAH = false>
-// 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
-// (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    TSAH || (MODE == MODE_MIXED && SCAN == SCAN_DEFER) ? 5 : 6))) void k_trace(const KParams P) {
-    trace_queue<MODE, SCAN, TSAH, false>(P);
-}
-// The linear sphere scan's frame-block refill with work stealing (rt_params.steal; short launches: a C2 job on the glass
-// sphere takes up to 1.7 ms, longer than a 1/8 share's whole launch)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_trace_steal(const KParams P) {
-    trace_queue<MODE_SPHERE, SCAN_SIMPLE, false, true>(P);
-}
 
 // Frame-block refill with the block in LDS (k_trace_split_tris; k_trace_split has the same code inline, which
 // compiles spill-free there): when the wave's block (one frame
@@ -3262,12 +3245,6 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
     } else if constexpr (MODE == MODE_TRIS) {
         return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
     } else {
-        if constexpr (MODE == MODE_SPHERE && !TSAH) {  // (the frame-block refill: work stealing, rt_params.steal)
-            if (variant == SCAN_SIMPLE && P.steal) {
-                snprintf(g_kernel_name, sizeof g_kernel_name, "k_trace_steal");
-                return launch_persistent(k_trace_steal, P, stream, g_kernel_name);
-            }
-        }
         if (variant == SCAN_SIMPLE) return launch_persistent(k_trace<MODE, SCAN_SIMPLE, TSAH>, P, stream, kname("k_trace", MODE, SCAN_SIMPLE, (int)TSAH));
         if (variant == SCAN_DEFER) return launch_persistent(k_trace<MODE, SCAN_DEFER, TSAH>, P, stream, kname("k_trace", MODE, SCAN_DEFER, (int)TSAH));
         if constexpr (MODE == MODE_SPHERE) {

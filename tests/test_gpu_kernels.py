@@ -64,7 +64,6 @@ def _cases():
                 cases.append((sd, dict(schedule=Q, steal=steal, count_tests=count)))
     for v in (1, 3):
         cases.append((c3, dict(schedule=Q, variant=v, steal=1)))
-    cases.append((c3, dict(schedule=Q, variant=1, steal=2)))  # k_trace_steal
     for v in (1, 3, 4):
         cases.append((c3, dict(schedule=T, variant=v)))
     for sd in (tris, c4, defer, bvh):

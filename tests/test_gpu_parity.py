@@ -687,7 +687,7 @@ def test_cost_order_bit_identical(steal, co):
         r = scenes.make_renderer(sd)
         # small colour budget: launches of ~7 frames, so the first draw already has ordered launches
         r.set_params(cost_order=co, queue_budget_mb=budget(sd) if sd.frames > 16 else 0, **base)
-        on = co >= 2 or (extra.get("row_step", 1) > 1 and steal == 1)  # (steal 2: every queue kernel here steals)
+        on = co >= 2 or (extra.get("row_step", 1) > 1 and (steal == 1 or sd.mode == hrt.RT_MODE_SPHERE and extra.get("variant") == 1))  # (k_trace never steals)
         for k in range(2):
             r.reset_frame_count()
             r.draw_frames(sd.frames, 1000, 10)
