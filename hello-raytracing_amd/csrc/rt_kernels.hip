@@ -1753,17 +1753,15 @@ __device__ __forceinline__ void job_account(const WaveJobs& J, bool fin, uint32_
 // stays far below its field's end). Wave state in the WaveJobs words the sample buffer leaves unused: flags (own
 // job, queue drained, lost race), the last victim, and the claimed frames not dealt yet.
 #ifndef HRT_STEAL_OWN
-#define HRT_STEAL_OWN 1  // (4 before round 5: the owner's claims of 4 frames held them from idle thieves in the tail)
+#define HRT_STEAL_OWN 1  // (4 before round 5: the owner's claims of 4 frames held them from idle thieves in the tail;
+                         // 4 only for jobs dealt early, while the queue holds > 2 jobs per wave: C4 8-way 0.756 -> 0.70,
+                         // the early jobs still running at the drain are the long ones, profiles/r05/p/)
 #endif
 #ifndef HRT_CLAIM_FREE
 #define HRT_CLAIM_FREE 32
 #endif
 constexpr uint32_t STEAL_OWN = HRT_STEAL_OWN;
-#ifndef HRT_STEAL_OWN_EARLY
-#define HRT_STEAL_OWN_EARLY 4
-#endif
-constexpr uint32_t STEAL_OWN_EARLY = HRT_STEAL_OWN_EARLY;
-constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u, ST_EARLY = 8u;
+constexpr uint32_t ST_OWN = 1u, ST_QEMPTY = 2u, ST_RETRY = 4u;
 // The tail (round 5): once the job queue is drained, a wave whose lanes are not all free claims another frame block only
 // when at least CLAIM_FREE of them are. A block claimed for a few free lanes waits for this wave's busy ones (paths of
 // up to 50 bounces) while other waves have run dry and exited: C4's 1/8 share drained its queue at 18.1 ms and ran to
@@ -1862,32 +1860,25 @@ __device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t la
     const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t st = J.get(WJ_ST);
     if (st & ST_OWN) {
-        const uint32_t own = st & ST_EARLY ? STEAL_OWN_EARLY : STEAL_OWN;
-        if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)own), own);
+        if (lane == 0) claim_publish(J, K, atomicAdd(slots + wid, (unsigned long long)STEAL_OWN), STEAL_OWN);
         if (claim_read(J, tile, frame)) return true;
-        J.set(WJ_ST, st & ~(ST_OWN | ST_EARLY));
+        J.set(WJ_ST, st & ~ST_OWN);
     }
     if (!(st & ST_QEMPTY)) {
-        uint32_t early = 0;
         if (lane == 0) {
             const uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
             unsigned long long v = 0;
-            // a job dealt early (more than two jobs per wave still queued behind it) is claimed STEAL_OWN_EARLY frames
-            // at a time: no thief comes before the queue drains, and a claim per frame block stalls the wave
-            early = (unsigned long long)j + 2ull * K->nwaves < K->njobs ? 1u : 0u;
-            const uint32_t own = early ? STEAL_OWN_EARLY : STEAL_OWN;
-            if (j < K->njobs) {  // the new job's first `own` frames are ours with the exchange
+            if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
                 const uint32_t tj = j / K->nchunks, c = j - tj * K->nchunks;
                 const uint32_t t = K->tile_order ? K->tile_order[tj] : tj;
                 const uint32_t nf = min(K->job_frames, K->nframes - c * K->job_frames);
                 v = ((unsigned long long)(t + 1u) << 39) | ((unsigned long long)c << 28) | ((unsigned long long)nf << 16);
-                (void)atomicExch(slots + wid, v + own);
+                (void)atomicExch(slots + wid, v + STEAL_OWN);
             }
-            claim_publish(J, K, v, own);
+            claim_publish(J, K, v, STEAL_OWN);
         }
-        early = uniform(__shfl(early, 0));
         if (claim_read(J, tile, frame)) {
-            J.set(WJ_ST, ST_OWN | (early ? ST_EARLY : 0u));
+            J.set(WJ_ST, ST_OWN);
             return true;
         }
     }
