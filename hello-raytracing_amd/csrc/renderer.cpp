@@ -178,6 +178,7 @@ struct rt_renderer {
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
     DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
+    DevBuf<unsigned long long> queues;       // sample buffer: the per-XCD job counters (rt_kernels.hip queue_take_lane0)
     uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
@@ -218,7 +219,7 @@ struct rt_renderer {
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
                tri_geo.bytes() + mats.bytes() +
                tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
-               wave_trace.bytes() + steal_slots.bytes() + tile_cost.bytes() + tile_sum.bytes() + tile_order.bytes() +
+               wave_trace.bytes() + steal_slots.bytes() + queues.bytes() + tile_cost.bytes() + tile_sum.bytes() + tile_order.bytes() +
                order_scratch.bytes();
     }
     uint32_t local_rows() const { return local_rows_of(height, params.row0, params.row_step, row_block()); }
@@ -707,6 +708,17 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // shares) 0.757 -> 0.739. Bit-identical in any order.
         const bool order_any = !P.ring_mode && r->params.cost_order != 1u;
         P.queue = r->counter.ptr + 15u;
+        // the sample buffer's jobs from one counter per XCD (HRT_NQ 0: the single counter)
+#ifndef HRT_NQ
+#define HRT_NQ 1
+#endif
+        constexpr size_t QWORDS = 8u * 16u;  // NQ x QSTRIDE
+        P.queues = nullptr;
+        if (HRT_NQ && !P.ring_mode) {
+            rc = ensure(r->queues, QWORDS);
+            if (rc) return rc;
+            P.queues = r->queues.ptr;
+        }
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
         r->last_suspend = split ? r->params.suspend_below : 0u;
@@ -746,6 +758,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             }
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
+            if (P.queues) HIP_TRY(hipMemsetAsync(P.queues, 0, QWORDS * sizeof(unsigned long long), r->stream));
             if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
             if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));
             rc = trace_events(r, r->trace_pairs_pending);
@@ -897,6 +910,7 @@ void delete_buffers(rt_renderer* r) {
     r->tb_order.release();
     r->counter.release();
     r->steal_slots.release();
+    r->queues.release();
     r->samples.release();
     r->ring.release();
     r->ring_ctl.release();

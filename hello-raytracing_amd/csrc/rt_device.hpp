@@ -158,6 +158,8 @@ struct KParams {
     uint32_t ring_bytes;          // size of `ring` (buffer-descriptor range)
     uint32_t jf_log2, pad_r;      // job_frames = 1 << jf_log2
     unsigned long long* queue;    // next job index (zeroed before each k_trace launch)
+    // sample buffer: NQ job counters, one per XCD, QSTRIDE words apart (rt_kernels.hip queue_take; null: `queue` alone)
+    unsigned long long* queues;
     unsigned long long njobs;     // tiles_w * tiles_h * ceil(nframes / job_frames), + 3 per job split in quarters
     uint32_t tail_from;           // sample buffer: jobs from this index on are parts of jobs (2^tail_shift per job)
     uint32_t tail_shift;

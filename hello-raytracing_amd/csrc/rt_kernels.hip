@@ -1622,6 +1622,31 @@ __device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uin
     return true;
 }
 
+// The sample buffer's job queue: NQ counters (renderer.cpp), queue q handing out the jobs k * NQ + q; a wave takes from
+// its XCD's queue first, then from the others in turn (the queues it found exhausted kept in its WJ_QDEAD word: the
+// ring's slot words, unused with the sample buffer). With one counter for the whole GPU every job fetch is an atomic
+// on one address from every XCD. Lane 0; returns >= njobs when every queue is exhausted.
+constexpr uint32_t NQ = 8, QSTRIDE = 16, WJ_QDEAD = WJ_SLOT;
+__device__ __forceinline__ uint32_t queue_take_lane0(const WaveJobs& J, const KPtr K) {
+    unsigned long long* const qs = K->queues;
+    if (qs == nullptr) return (uint32_t)min(atomicAdd(K->queue, 1ull), 0xFFFFFFFFull);
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    uint32_t dead = J.w[WJ_QDEAD], j = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < NQ; i++) {
+        const uint32_t q = (x + i) & (NQ - 1u);
+        if ((dead >> q) & 1u) continue;
+        const unsigned long long jj = atomicAdd(qs + q * QSTRIDE, 1ull) * NQ + q;
+        if (jj < K->njobs) {
+            j = (uint32_t)jj;
+            break;
+        }
+        dead |= 1u << q;
+    }
+    J.w[WJ_QDEAD] = dead;
+    return j;
+}
+
 // Makes a job current and dealable: fetch one into a free entry and wait for its slot.
 // false: nothing to deal now (queue drained -> `drained`; every entry still in flight; slot still folding).
 // TAIL: the sample buffer's quarter jobs at the end of the launch (renderer.cpp tail_from; k_trace_split only:
@@ -1633,7 +1658,7 @@ __device__ __forceinline__ bool job_acquire(const WaveJobs& J, uint32_t lane, bo
     uint32_t flags = J.get(WJ_FLAGS);
     if (!K->ring_mode) {  // sample buffer: no entries, no slots
         uint32_t j = 0;
-        if (lane == 0) j = (uint32_t)atomicAdd(K->queue, 1ull);
+        if (lane == 0) j = queue_take_lane0(J, K);
         j = uniform(__shfl(j, 0));
         if (j >= K->njobs) {
             drained = true;
@@ -1781,11 +1806,15 @@ enum : uint32_t { WJ_ST = WJ_TILE, WJ_VICTIM = WJ_TILE + 1, WJ_PRIV_F = WJ_TILE 
 // true when the job queue is drained (known to this wave, or read from the queue counter: one load per call)
 __device__ __forceinline__ bool queue_drained(const WaveJobs& J, uint32_t lane) {
     if (J.get(WJ_ST) & ST_QEMPTY) return true;
-    uint32_t d = 0;
-    if (lane == 0) {
-        const KPtr K = kargs();
-        d = __hip_atomic_load(K->queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= K->njobs ? 1u : 0u;
+    const KPtr K = kargs();
+    if (unsigned long long* const qs = K->queues) {  // every queue exhausted (lane q reads queue q)
+        bool done = true;
+        if (lane < NQ)
+            done = __hip_atomic_load(qs + lane * QSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * NQ + lane >= K->njobs;
+        return __ballot(!done) == 0ull;
     }
+    uint32_t d = 0;
+    if (lane == 0) d = __hip_atomic_load(K->queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= K->njobs ? 1u : 0u;
     return uniform(__shfl(d, 0)) != 0u;
 }
 
@@ -1866,7 +1895,7 @@ __device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t la
     }
     if (!(st & ST_QEMPTY)) {
         if (lane == 0) {
-            const uint32_t j = (uint32_t)atomicAdd(K->queue, 1ull);
+            const uint32_t j = queue_take_lane0(J, K);
             unsigned long long v = 0;
             if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
                 const uint32_t tj = j / K->nchunks, c = j - tj * K->nchunks;
