@@ -88,10 +88,12 @@ def main() -> None:
     ap.add_argument("--rank", type=int, nargs="+", default=[4])
     ap.add_argument("--steal", type=int, default=None)
     ap.add_argument("--full", action="store_true", help="also the full image")
+    ap.add_argument("--param", action="append", default=[], help="extra rt_params field=value (repeatable)")
     a = ap.parse_args()
     assert hrt.lib().rt_diagnostic_build() == 1, "run with HRT_LIB=lib/libhrt_diag.so"
     sd = scenes.CONFIGS[a.config]()
     extra = {} if a.steal is None else {"steal": a.steal}
+    extra.update({k: int(v) for k, v in (p.split("=", 1) for p in a.param)})
     res = {}
     for k in a.rank:
         res[f"rank{k}of{a.ranks}"] = draw(sd, {**rank_params(k, a.ranks, 8), **bench.timed_knobs(**extra)})
