@@ -2978,13 +2978,13 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 
 // Cost-ordered dealing (rt_params.cost_order; renderer.cpp): a learning launch sums its samples' queries per pixel
 // (pixel_cost, ring_store); the tiles are then split into a head — the most expensive ones, at most ORDER_HEAD_PCT % of
-// them, by log-scale cost classes — and the rest, each in raster order, and later launches deal the head first
-// (job_acquire, steal_block_claim: tile_order[job / nchunks]). A tile whose paths bounce up to the cap costs many
-// times a sky tile; dealt late, its jobs outlast the launch. A full sort by cost measured slower: the GPU then works on
-// tiles from all over the image at once (C4 -2.3 %, C2 -5 %, C3 -0.8 % on full images: the rays of a band of adjacent
-// tiles share their scene data in the caches), and the head keeps raster order among the expensive tiles, which
-// cluster on the same objects. Which wave traces a sample never changes its colour or its place in the sample buffer,
-// so the image is bit-identical in any order.
+// them, by log-scale cost classes — sorted by class, most expensive first (raster order within a class at the grain of
+// ORDER_BLOCK tiles), and the rest in raster order; later launches deal the head first (job_acquire, steal_block_claim:
+// tile_order[job / nchunks]). A tile whose paths bounce up to the cap costs many times a sky tile; dealt late, its jobs
+// outlast the launch. A full sort by cost measured slower: the GPU then works on tiles from all over the image at once
+// (C4 -2.3 %, C2 -5 %, C3 -0.8 % on full images: the rays of a band of adjacent tiles share their scene data in the
+// caches); the head's expensive tiles cluster on the same objects. Which wave traces a sample never changes its colour
+// or its place in the sample buffer, so the image is bit-identical in any order.
 constexpr uint32_t ORDER_BUCKETS = 128, ORDER_HEAD_PCT = 25, ORDER_BLOCK = 1024;
 __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
     // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, <= 2^32: the
@@ -2993,8 +2993,13 @@ __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
     return (ORDER_BUCKETS - 1u) - min(k, ORDER_BUCKETS - 1u);
 }
 // scratch words: [0, 128) class histogram (zero between sorts), [128] the head's classes (class < cut), [129] head
-// size, [256, 256 + blocks) head tiles per ORDER_BLOCK tiles, then their exclusive prefix sums
-constexpr uint32_t OS_HIST = 0, OS_CUT = ORDER_BUCKETS, OS_NHEAD = ORDER_BUCKETS + 1, OS_BLK = 2 * ORDER_BUCKETS;
+// size, [256, 384) the head classes' first positions, [384, 384 + blocks) head tiles per ORDER_BLOCK tiles, then their
+// exclusive prefix sums, then blocks x 128 head tiles per block and class, then the positions where they go
+constexpr uint32_t OS_HIST = 0, OS_CUT = ORDER_BUCKETS, OS_NHEAD = ORDER_BUCKETS + 1, OS_CBASE = 2 * ORDER_BUCKETS,
+                   OS_BLK = 3 * ORDER_BUCKETS;
+__device__ __forceinline__ uint32_t os_cls(uint32_t nblocks, uint32_t blk, uint32_t c) {
+    return OS_BLK + nblocks + blk * ORDER_BUCKETS + c;
+}
 // one wave per tile: the tile's 64 pixel counters summed (saturating) into tile_sum and zeroed for the next learning
 // launch, the tile's class counted
 __global__ __launch_bounds__(256) void k_order_hist(uint32_t* __restrict__ pixel_cost, uint32_t ntiles,
@@ -3029,6 +3034,7 @@ __global__ void k_order_cut(uint32_t* scratch, uint32_t ntiles) {
         const uint32_t c = scratch[OS_HIST + b];
         scratch[OS_HIST + b] = 0u;
         if (open && n + c <= cap) {
+            scratch[OS_CBASE + b] = n;
             n += c;
             cut = b + 1u;
         } else {
@@ -3038,22 +3044,31 @@ __global__ void k_order_cut(uint32_t* scratch, uint32_t ntiles) {
     scratch[OS_CUT] = cut;
     scratch[OS_NHEAD] = n;
 }
-__device__ __forceinline__ bool order_head(const uint32_t* tile_sum, const uint32_t* scratch, uint32_t t) {
-    return order_bucket(tile_sum[t]) < scratch[OS_CUT];
-}
-// head tiles per block of ORDER_BLOCK tiles (256 threads x 4 tiles)
-__global__ __launch_bounds__(256) void k_order_count(const uint32_t* __restrict__ tile_sum, uint32_t ntiles, uint32_t* scratch) {
+// head tiles per block of ORDER_BLOCK tiles (256 threads x 4 tiles), in all and per class
+__global__ __launch_bounds__(256) void k_order_count(const uint32_t* __restrict__ tile_sum, uint32_t ntiles, uint32_t* scratch,
+                                                     uint32_t nblocks) {
+    __shared__ uint32_t h[ORDER_BUCKETS];
+    __shared__ uint32_t w[4];
+    for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) h[b] = 0u;
+    __syncthreads();
+    const uint32_t cut = scratch[OS_CUT];
     uint32_t c = 0;
     for (uint32_t k = 0; k < 4u; k++) {
         const uint32_t t = blockIdx.x * ORDER_BLOCK + k * 256u + threadIdx.x;
-        c += t < ntiles && order_head(tile_sum, scratch, t) ? 1u : 0u;
+        if (t < ntiles) {
+            const uint32_t cls = order_bucket(tile_sum[t]);
+            if (cls < cut) {
+                c++;
+                atomicAdd(&h[cls], 1u);
+            }
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    __shared__ uint32_t w[4];
     if ((threadIdx.x & 63u) == 0u) w[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) scratch[OS_BLK + blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+    for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) scratch[os_cls(nblocks, blockIdx.x, b)] = h[b];
 }
 // one workgroup: exclusive prefix sums of the blocks' head counts, in place (nblocks <= 2^15)
 __global__ __launch_bounds__(1024) void k_order_blockscan(uint32_t* scratch, uint32_t nblocks) {
@@ -3075,23 +3090,39 @@ __global__ __launch_bounds__(1024) void k_order_blockscan(uint32_t* scratch, uin
         scratch[OS_BLK + b0 + k] = run;
         run += c;
     }
+    // the head classes: a class's tiles go to its first position onwards, block by block
+    const uint32_t cls = threadIdx.x;
+    if (cls < scratch[OS_CUT]) {
+        uint32_t pos = scratch[OS_CBASE + cls];
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const uint32_t i = os_cls(nblocks, b, cls), n = scratch[i];
+            scratch[i] = pos;
+            pos += n;
+        }
+    }
 }
-// stable partition: head tiles to [0, nhead) and the others to [nhead, ntiles), each in tile order
+// head tiles to [0, nhead) by class (most expensive first; within a class block by block), the others to
+// [nhead, ntiles) in tile order
 __global__ __launch_bounds__(256) void k_order_scatter(const uint32_t* __restrict__ tile_sum, uint32_t ntiles,
-                                                       const uint32_t* scratch, uint32_t* __restrict__ order) {
+                                                       const uint32_t* scratch, uint32_t* __restrict__ order, uint32_t nblocks) {
     __shared__ uint32_t w[4];
-    const uint32_t nhead = scratch[OS_NHEAD];
+    __shared__ uint32_t next[ORDER_BUCKETS];
+    for (uint32_t b = threadIdx.x; b < ORDER_BUCKETS; b += 256u) next[b] = scratch[os_cls(nblocks, blockIdx.x, b)];
+    __syncthreads();
+    const uint32_t nhead = scratch[OS_NHEAD], cut = scratch[OS_CUT];
     uint32_t before = scratch[OS_BLK + blockIdx.x];  // head tiles before this block's current group of 256
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     for (uint32_t k = 0; k < 4u; k++) {
         const uint32_t t = blockIdx.x * ORDER_BLOCK + k * 256u + threadIdx.x;
-        const bool h = t < ntiles && order_head(tile_sum, scratch, t);
+        const uint32_t cls = t < ntiles ? order_bucket(tile_sum[t]) : ORDER_BUCKETS;
+        const bool h = cls < cut;
         const unsigned long long m = __ballot(h);
         if (lane == 0u) w[wv] = (uint32_t)__popcll(m);
         __syncthreads();
         uint32_t r = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         for (uint32_t q = 0; q < wv; q++) r += w[q];
-        if (t < ntiles) order[h ? r : nhead + (t - r)] = t;
+        if (h) order[atomicAdd(&next[cls], 1u)] = t;
+        else if (t < ntiles) order[nhead + (t - r)] = t;
         before += w[0] + w[1] + w[2] + w[3];
         __syncthreads();
     }
@@ -3104,12 +3135,15 @@ hipError_t hrt_launch_order(uint32_t* pixel_cost, uint32_t ntiles, uint32_t* til
     if (nblocks > 32768u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_order_hist, dim3((ntiles + 3u) / 4u), dim3(256), 0, stream, pixel_cost, ntiles, tile_sum, scratch);
     hipLaunchKernelGGL(k_order_cut, dim3(1), dim3(64), 0, stream, scratch, ntiles);
-    hipLaunchKernelGGL(k_order_count, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch);
+    hipLaunchKernelGGL(k_order_count, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch, nblocks);
     hipLaunchKernelGGL(k_order_blockscan, dim3(1), dim3(1024), 0, stream, scratch, nblocks);
-    hipLaunchKernelGGL(k_order_scatter, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch, order);
+    hipLaunchKernelGGL(k_order_scatter, dim3(nblocks), dim3(256), 0, stream, tile_sum, ntiles, scratch, order, nblocks);
     return hipGetLastError();
 }
-uint32_t hrt_order_scratch_words(uint32_t ntiles) { return OS_BLK + (ntiles + ORDER_BLOCK - 1u) / ORDER_BLOCK; }
+uint32_t hrt_order_scratch_words(uint32_t ntiles) {
+    const uint32_t nblocks = (ntiles + ORDER_BLOCK - 1u) / ORDER_BLOCK;
+    return OS_BLK + nblocks + nblocks * ORDER_BUCKETS;
+}
 
 // Exactness check of the range-restricted sqrt / division sequences (rt_device.hpp) against the IEEE
 // operations (correctly rounded in this build): n random cases per test, counted mismatches in out[0..2]:
