@@ -699,14 +699,25 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         if (rc) return rc;
         P.steal_slots = r->steal_slots.ptr;
         // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): a learning launch counts its samples'
-        // queries per pixel and the tiles are split into the most expensive quarter and the rest; the following launches
-        // (of this draw and the next ones) deal that head first, each part in raster order, so the jobs that take
-        // longest start early instead of trailing the launch. The renderer learns in its first ordered launch after any
-        // scene, camera, size or parameter change (cost_order 3: in every launch). Auto: a rank's share of a row
-        // partition (row_step > 1) without stealing — measured (profiles/r05/l/): 8-way splits C3 0.940 -> 0.960,
-        // C5 0.974 -> 0.987, C2 0.52 -> 0.59; full images C3 -0.2 %, C4 -0.6 %, C2 -2.3 %; with stealing (C4's
-        // shares) 0.757 -> 0.739. Bit-identical in any order.
+        // queries per pixel and the tiles are split into the most expensive quarter, sorted by cost, and the rest in
+        // raster order; the following launches (of this draw and the next ones) deal that head first, so the jobs that
+        // take longest start early instead of trailing the launch. The renderer learns in its first ordered launch after
+        // any scene, camera, size or parameter change (cost_order 3: in every launch). Auto: a rank's share of a row
+        // partition (row_step > 1), which then does not steal — measured (profiles/r05/l/, t/): 8-way splits C3 0.940 ->
+        // 0.957, C5 0.974 -> 0.987, C2 0.52 -> 0.68 and C4 0.755 -> 0.82 with the short-launch job size below; full
+        // images C3 -0.2 %, C4 -0.6 %, C2 -2.3 %. Bit-identical in any order.
         const bool order_any = !P.ring_mode && r->params.cost_order != 1u;
+        const bool want_order = order_any && (r->params.cost_order >= 2u || r->params.row_step > 1u);
+        // Short launches (a rank's share of a row partition, small images): fewer than 32 jobs per resident wave at the
+        // kernel's job size. Their jobs are halved (job_frames 0 only), so a job on a costly tile no longer outlasts the
+        // launch: C4's 8-way shares in cost order 0.43 with 32-frame jobs, 0.82 with 16; C2's shares 1.00 ms with 8-frame
+        // jobs against 1.16 with 16, C3's flat (profiles/r05/r/, t/). Long launches keep the larger jobs (C2 full image
+        // -2.6 % with 8, C4 -1.2 % with 16).
+        if (!P.ring_mode && r->params.job_frames == 0u && jf > 1u &&
+            (uint64_t)ntiles * ((chunk + jf - 1u) / jf) < 32ull * 24u * std::max(r->cus, 1u)) {
+            jf >>= 1;
+            P.jf_log2--;
+        }
         P.queue = r->counter.ptr + 15u;
         // the sample buffer's jobs from one counter per XCD (HRT_NQ 0: the single counter)
 #ifndef HRT_NQ
@@ -736,8 +747,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             // 0.88)
             {
                 const bool fits = ntiles < (1u << 25) - 1u && P.nchunks < 2048u;  // the slot's tile and chunk fields
+                // (not once the launch can deal in cost order: C4's 8-way shares 0.755 with stealing, 0.82 in order)
                 const bool want = r->params.steal == 2u ||
-                                  (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u));
+                                  (r->params.steal == 0u && P.njobs < 16ull * 24u * std::max(r->cus, 1u) &&
+                                   !(want_order && r->order_tiles == ntiles));
                 // (k_trace's frame-block refill for the linear sphere scan with the same stealing ran 3x slower, C2 80 ->
                 // 26 Grays/s: a claim per 64 cheap samples stalls the wave; profiles/r05/o/)
                 P.steal = (split && !P.ring_mode && fits && want) ? 1u : 0u;
@@ -764,9 +777,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             rc = trace_events(r, r->trace_pairs_pending);
             if (rc) return rc;
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending], r->stream));
-            const bool order_on =
-                order_any && (r->params.cost_order >= 2u || (r->params.row_step > 1u && !P.steal));
-            if (order_on && r->cost_tiles != ntiles) {
+            const bool order_on = want_order && (r->params.cost_order >= 2u || !P.steal);
+            if (want_order && r->cost_tiles != ntiles) {
                 const size_t SCRATCH = hrt_order_scratch_words(ntiles);
                 rc = ensure(r->tile_cost, (size_t)ntiles * 64u);
                 if (!rc) rc = ensure(r->tile_sum, ntiles);
@@ -781,7 +793,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             }
             P.tile_order = order_on && r->order_tiles == ntiles ? r->tile_order.ptr : nullptr;
             ordered += P.tile_order ? 1u : 0u;
-            const bool learn = order_on && (r->cost_learn || r->params.cost_order == 3u);
+            // (a launch that steals still learns, so the next one can deal in cost order instead)
+            const bool learn = want_order && (r->cost_learn || r->params.cost_order == 3u);
             P.tile_cost = learn ? r->tile_cost.ptr : nullptr;
             HIP_TRY(hrt_launch_trace(r->mode, variant, P, r->stream));
             HIP_TRY(hipEventRecord(r->ev_trace[2 * r->trace_pairs_pending + 1], r->stream));
