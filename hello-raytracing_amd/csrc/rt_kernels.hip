@@ -2985,7 +2985,10 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 // (C4 -2.3 %, C2 -5 %, C3 -0.8 % on full images: the rays of a band of adjacent tiles share their scene data in the
 // caches); the head's expensive tiles cluster on the same objects. Which wave traces a sample never changes its colour
 // or its place in the sample buffer, so the image is bit-identical in any order.
-constexpr uint32_t ORDER_BUCKETS = 128, ORDER_HEAD_PCT = 25, ORDER_BLOCK = 1024;
+#ifndef HRT_ORDER_HEAD_PCT
+#define HRT_ORDER_HEAD_PCT 25
+#endif
+constexpr uint32_t ORDER_BUCKETS = 128, ORDER_HEAD_PCT = HRT_ORDER_HEAD_PCT, ORDER_BLOCK = 1024;
 __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {
     // floor(4 * log2(cost + 1)) from the float's exponent and top two significand bits (cost + 1 >= 1, <= 2^32: the
     // class of 2^32 is clamped), most expensive first
