@@ -699,7 +699,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         if (rc) return rc;
         P.steal_slots = r->steal_slots.ptr;
         // Cost-ordered dealing (rt_params.cost_order; rt_kernels.hip k_order_*): a learning launch counts its samples'
-        // queries per pixel and the tiles are split into the most expensive quarter, sorted by cost, and the rest in
+        // queries per pixel and the tiles are split into the most expensive half, sorted by cost, and the rest in
         // raster order; the following launches (of this draw and the next ones) deal that head first, so the jobs that
         // take longest start early instead of trailing the launch. The renderer learns in its first ordered launch after
         // any scene, camera, size or parameter change (cost_order 3: in every launch). Auto: a rank's share of a row

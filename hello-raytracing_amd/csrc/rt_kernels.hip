@@ -2977,7 +2977,7 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 }
 
 // Cost-ordered dealing (rt_params.cost_order; renderer.cpp): a learning launch sums its samples' queries per pixel
-// (pixel_cost, ring_store); the tiles are then split into a head — the most expensive ones, at most ORDER_HEAD_PCT % of
+// (pixel_cost, ring_store); the tiles are then split into a head — the most expensive ones, at most ORDER_HEAD_PCT (50) % of
 // them, by log-scale cost classes — sorted by class, most expensive first (raster order within a class at the grain of
 // ORDER_BLOCK tiles), and the rest in raster order; later launches deal the head first (job_acquire, steal_block_claim:
 // tile_order[job / nchunks]). A tile whose paths bounce up to the cap costs many times a sky tile; dealt late, its jobs
@@ -2986,7 +2986,7 @@ hipError_t hrt_launch_accumulate(const KParams& P, hipStream_t stream) {
 // caches); the head's expensive tiles cluster on the same objects. Which wave traces a sample never changes its colour
 // or its place in the sample buffer, so the image is bit-identical in any order.
 #ifndef HRT_ORDER_HEAD_PCT
-#define HRT_ORDER_HEAD_PCT 25
+#define HRT_ORDER_HEAD_PCT 50  // (12 / 25 / 50 / 100: C4 8-way 0.82 / 0.82 / 0.84 / 0.83, C2 0.66 / 0.65 / 0.66 / 0.65; profiles/r05/v/)
 #endif
 constexpr uint32_t ORDER_BUCKETS = 128, ORDER_HEAD_PCT = HRT_ORDER_HEAD_PCT, ORDER_BLOCK = 1024;
 __device__ __forceinline__ uint32_t order_bucket(uint32_t cost) {

@@ -116,12 +116,12 @@ typedef struct rt_params {
                                   k_trace_split does not count them (reported 0; 1.3 % of C3's kernel
                                   time); the other kernels always count                                  */
     uint32_t cost_order;       /* sample queue with the sample buffer: deal a launch's most expensive tiles first
-                                  (a quarter of them, by the queries their samples took in a learning launch;
-                                  then the rest; each part in raster order), so the slowest jobs do not trail
+                                  (half of them, sorted by the queries their samples took in a learning launch;
+                                  then the rest in raster order), so the slowest jobs do not trail
                                   the launch. The first ordered launch after a change of scene, camera, size or
                                   parameters learns (and deals in the last order learnt, or raster order).
-                                  0 auto = on for a rank's share of a row partition (row_step > 1) when the
-                                  launch does not steal, 1 off, 2 on, 3 on with every launch learning;
+                                  0 auto = on for a rank's share of a row partition (row_step > 1), which then
+                                  does not steal once it has learnt, 1 off, 2 on, 3 on with every launch learning;
                                   bit-identical always                           */
 } rt_params;
 

@@ -664,7 +664,7 @@ def test_work_stealing_bit_identical(jf):
 @pytest.mark.parametrize("steal,co", [(1, 3), (2, 3), (1, 2), (1, 0), (2, 0)])
 def test_cost_order_bit_identical(steal, co):
     """Cost-ordered dealing (rt_params.cost_order: 2 on, learning once; 3 on, learning in every launch; 0 auto = on for
-    a row partition's share without stealing): a launch deals the most expensive quarter of its tiles first (learnt from
+    a row partition's share without stealing): a launch deals the most expensive half of its tiles first (learnt from
     a launch's per-pixel query counts), then the rest. A renderer's first draw deals its first launch in raster order
     and the later launches in cost order, its second draw every launch in cost order; both give the images and ray /
     node / triangle counts of raster-order draws (cost_order 1) and of the oracle — sphere program (k_trace_split),
