@@ -728,7 +728,6 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         if (HRT_NQ && !P.ring_mode) {
             rc = ensure(r->queues, QWORDS);
             if (rc) return rc;
-            P.queues = r->queues.ptr;
         }
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
@@ -771,6 +770,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
             }
             r->ring_nchunks = P.nchunks;
             HIP_TRY(hipMemsetAsync(P.queue, 0, sizeof(unsigned long long), r->stream));
+            // (not with stealing: its launches are short, and the per-XCD fetch spilled SGPRs in the stealing kernels)
+            P.queues = HRT_NQ && !P.ring_mode && !P.steal ? r->queues.ptr : nullptr;
             if (P.queues) HIP_TRY(hipMemsetAsync(P.queues, 0, QWORDS * sizeof(unsigned long long), r->stream));
             if (P.steal) HIP_TRY(hipMemsetAsync(P.steal_slots, 0, P.steal_cap * sizeof(unsigned long long), r->stream));
             if (P.ring_mode) HIP_TRY(hipMemsetAsync(r->ring_ctl.ptr, 0, zero_words * sizeof(uint32_t), r->stream));

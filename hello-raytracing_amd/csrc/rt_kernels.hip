@@ -1895,7 +1895,8 @@ __device__ __forceinline__ bool steal_block_claim(const WaveJobs& J, uint32_t la
     }
     if (!(st & ST_QEMPTY)) {
         if (lane == 0) {
-            const uint32_t j = queue_take_lane0(J, K);
+            // (stealing launches fetch from the single counter: renderer.cpp passes no per-XCD queues with steal)
+            const uint32_t j = (uint32_t)min(atomicAdd(K->queue, 1ull), 0xFFFFFFFFull);
             unsigned long long v = 0;
             if (j < K->njobs) {  // the new job's first STEAL_OWN frames are ours with the exchange
                 const uint32_t tj = j / K->nchunks, c = j - tj * K->nchunks;
