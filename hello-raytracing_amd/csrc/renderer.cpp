@@ -702,7 +702,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // queries per pixel and the tiles are split into the most expensive half, sorted by cost, and the rest in
         // raster order; the following launches (of this draw and the next ones) deal that head first, so the jobs that
         // take longest start early instead of trailing the launch. The renderer learns in its first ordered launch after
-        // any scene, camera, size or parameter change (cost_order 3: in every launch). Auto: a rank's share of a row
+        // any scene, camera, size, row, bounce-cap, slot or triangle-walk change (cost_order 3: in every launch). Auto: a rank's share of a row
         // partition (row_step > 1), which then does not steal — measured (profiles/r05/l/, t/): 8-way splits C3 0.940 ->
         // 0.957, C5 0.974 -> 0.987, C2 0.52 -> 0.68 and C4 0.755 -> 0.82 with the short-launch job size below; full
         // images C3 -0.2 %, C4 -0.6 %, C2 -2.3 %. Bit-identical in any order.
@@ -1051,8 +1051,11 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||
                               std::max(p->row_block, 1u) != r->row_block();
     const bool slots_changed = p->min_sphere_slots != r->params.min_sphere_slots;
+    // the tiles' costs (queries per sample) change with the rows, the bounce cap and the scene's slots or triangle walk,
+    // not with the kernels' knobs (count_tests, job size, ...: bench.py toggles count_tests around every warmup step)
+    if (rows_changed || slots_changed || p->bounces != r->params.bounces || p->tri_bvh != r->params.tri_bvh)
+        r->cost_learn = true;
     r->params = *p;
-    r->cost_learn = true;
     if (rows_changed) {
         r->frame_count = 0;
         int rc = zero_image(r);

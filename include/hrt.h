@@ -118,8 +118,9 @@ typedef struct rt_params {
     uint32_t cost_order;       /* sample queue with the sample buffer: deal a launch's most expensive tiles first
                                   (half of them, sorted by the queries their samples took in a learning launch;
                                   then the rest in raster order), so the slowest jobs do not trail
-                                  the launch. The first ordered launch after a change of scene, camera, size or
-                                  parameters learns (and deals in the last order learnt, or raster order).
+                                  the launch. The first launch after a change of scene, camera, size, rows,
+                                  bounce cap, sphere slots or triangle walk learns (and deals in the last order
+                                  learnt, or raster order).
                                   0 auto = on for a rank's share of a row partition (row_step > 1), which then
                                   does not steal once it has learnt, 1 off, 2 on, 3 on with every launch learning;
                                   bit-identical always                           */
