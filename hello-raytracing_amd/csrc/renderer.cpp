@@ -702,12 +702,15 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // queries per pixel and the tiles are split into the most expensive half, sorted by cost, and the rest in
         // raster order; the following launches (of this draw and the next ones) deal that head first, so the jobs that
         // take longest start early instead of trailing the launch. The renderer learns in its first ordered launch after
-        // any scene, camera, size, row, bounce-cap, slot or triangle-walk change (cost_order 3: in every launch). Auto: a rank's share of a row
-        // partition (row_step > 1), which then does not steal — measured (profiles/r05/l/, t/): 8-way splits C3 0.940 ->
-        // 0.957, C5 0.974 -> 0.987, C2 0.52 -> 0.68 and C4 0.755 -> 0.82 with the short-launch job size below; full
-        // images C3 -0.2 %, C4 -0.6 %, C2 -2.3 %. Bit-identical in any order.
+        // any scene, camera, size, row, bounce-cap, slot or triangle-walk change (cost_order 3: in every launch).
+        // Auto: a rank's share of a row partition (row_step > 1), which then does not steal, and the suspendable-walk
+        // kernels' full images — measured (profiles/r05/t/, u/, y/): 8-way splits C3 0.940 -> 0.96, C5 0.974 -> 0.987,
+        // C2 0.52 -> 0.66 and C4 0.755 -> 0.84 with the short-launch job size below; full images C3 +0.6 %, C5 +0.3 %,
+        // C4 flat, C2 (k_trace, not ordered) -1.5 %. Bit-identical in any order.
         const bool order_any = !P.ring_mode && r->params.cost_order != 1u;
-        const bool want_order = order_any && (r->params.cost_order >= 2u || r->params.row_step > 1u);
+        // (full images too for the suspendable-walk kernels: C3 38.29 -> 38.53 Grays/s, C5 +0.3 %, C4 flat; not for
+        // k_trace's full images: C2 -1.5 %; profiles/r05/y/)
+        const bool want_order = order_any && (r->params.cost_order >= 2u || r->params.row_step > 1u || split);
         // Short launches (a rank's share of a row partition, small images): fewer than 32 jobs per resident wave at the
         // kernel's job size. Their jobs are halved (job_frames 0 only), so a job on a costly tile no longer outlasts the
         // launch: C4's 8-way shares in cost order 0.43 with 32-frame jobs, 0.82 with 16; C2's shares 1.00 ms with 8-frame

@@ -122,7 +122,8 @@ typedef struct rt_params {
                                   bounce cap, sphere slots or triangle walk learns (and deals in the last order
                                   learnt, or raster order).
                                   0 auto = on for a rank's share of a row partition (row_step > 1), which then
-                                  does not steal once it has learnt, 1 off, 2 on, 3 on with every launch learning;
+                                  does not steal once it has learnt, and for the suspendable-walk kernels (not
+                                  the linear scans' full images), 1 off, 2 on, 3 on with every launch learning;
                                   bit-identical always                           */
 } rt_params;
 

@@ -664,7 +664,8 @@ def test_work_stealing_bit_identical(jf):
 @pytest.mark.parametrize("steal,co", [(1, 3), (2, 3), (1, 2), (1, 0), (2, 0)])
 def test_cost_order_bit_identical(steal, co):
     """Cost-ordered dealing (rt_params.cost_order: 2 on, learning once; 3 on, learning in every launch; 0 auto = on for
-    a row partition's share without stealing): a launch deals the most expensive half of its tiles first (learnt from
+    a row partition's share and the suspendable-walk kernels, when not stealing): a launch deals the most expensive half
+    of its tiles first (learnt from
     a launch's per-pixel query counts), then the rest. A renderer's first draw deals its first launch in raster order
     and the later launches in cost order, its second draw every launch in cost order; both give the images and ray /
     node / triangle counts of raster-order draws (cost_order 1) and of the oracle — sphere program (k_trace_split),
@@ -687,7 +688,8 @@ def test_cost_order_bit_identical(steal, co):
         r = scenes.make_renderer(sd)
         # small colour budget: launches of ~7 frames, so the first draw already has ordered launches
         r.set_params(cost_order=co, queue_budget_mb=budget(sd) if sd.frames > 16 else 0, **base)
-        on = co >= 2 or (extra.get("row_step", 1) > 1 and (steal == 1 or sd.mode == hrt.RT_MODE_SPHERE and extra.get("variant") == 1))  # (k_trace never steals)
+        split = extra.get("variant") != 1  # (variant 1: the linear scan's k_trace, which never steals)
+        on = co >= 2 or ((steal == 1 or not split) and (extra.get("row_step", 1) > 1 or split))
         for k in range(2):
             r.reset_frame_count()
             r.draw_frames(sd.frames, 1000, 10)
