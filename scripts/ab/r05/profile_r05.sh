@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 profiles of C3 / C4 / C5 on the final tree: rocprofv3 kernel-trace stats + the PMC passes (scripts/profile_round.sh)
 # and the phase split of the diagnostic phase build (C3, C4, C5 at 16 frames; lib/libhrt_phase.so). Logs: gpurun_out/r05_*.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 bash scripts/profile_round.sh r05_c3 --config c3 --steps 3 --warmup 1 --emulate-ranks 0 &&
 bash scripts/profile_round.sh r05_c4 --config c4 --steps 3 --warmup 1 --emulate-ranks 0 &&
 bash scripts/profile_round.sh r05_c5 --config c5 --steps 1 --warmup 1 --emulate-ranks 0 &&

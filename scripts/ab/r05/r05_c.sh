@@ -2,7 +2,7 @@
 # Round-5 batch: the short-launch / walk-lane diagnostics (scripts/r05_tail.sh), then k_trace_split with 896-lane
 # workgroups (nodes in LDS; + leaf spheres in LDS) against the product build: C3 parity tests on the variant, then an
 # interleaved same-box A/B (scripts/ab_lib.sh). Logs: gpurun_out/<tag>/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05c}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/r05_tail.sh "$tag" || exit 1

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 check on one GPU: smoke, the new timed-configuration / instantiation tests, the full GPU suite, the default
 # bench line, and a two-rank gloo rehearsal of the multi-rank line (device fields, C5 leg). Logs: gpurun_out/<tag>/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05a}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/smoke" 300 python -c "import __graft_entry__ as g; g.smoke()" \

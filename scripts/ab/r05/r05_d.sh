@@ -2,7 +2,7 @@
 # Round-5 batch D: the triangle and tail-split parity tests on the product build (compact 36-B triangle operands,
 # tail parts in k_trace's frame-block refill), then same-box A/Bs: C4 / C5 (256 spp) against the 64-B triangle loads
 # (lib/libhrt_tri64.so), C2 with its 8-way split. Logs: gpurun_out/<tag>/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05d}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 600 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 batch E: C4's 8-way emulated split under the short-launch options (bench.py knobs apply to the full image and
 # to every share): stealing auto (default), stealing off (the tail split then applies), off + eighths, 16-frame jobs.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05e}"
 mkdir -p "gpurun_out/$tag"
 for v in "auto:" "nosteal:--steal 1" "nosteal8:--steal 1 --tail-split 3" "jf16:--job-frames 16" "jf16nosteal:--job-frames 16 --steal 1"; do

@@ -2,7 +2,7 @@
 # Round-5 batch F: parity tests on the product build (tail claim rule, compact triangle operands, k_trace tail parts),
 # then same-box A/Bs: C4's 8-way emulated split by tail claim rule (CLAIM_FREE 0 = round 4 / 32 = product / 48; STEAL_OWN 1),
 # the compact triangle operands on C4 / C5 (256 spp), C2 with / without tail parts; then the WRITE_SIZE calibration.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05f}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 final check A: the whole GPU suite, smoke(), the default bench line (the driver's command) on the final tree,
 # and the diagnostic build's wave records of 1/8 C2 and C4 shares with the final defaults.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05_final}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests_gpu" 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread || exit 1

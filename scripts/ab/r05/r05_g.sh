@@ -3,7 +3,7 @@
 # (lib/libhrt_tc0.so = HRT_TAIL_CLAIM=0, round 4) on C3, C4 without stealing and C5, with their 8-way emulated splits
 # (ab_lib.sh prints: value, ms/step, emulated efficiency, predicted ms/step); then C4's 8-way split under the
 # short-launch options (the bench knobs apply to the full image and every share) and the wave records of a 1/8 C4 share.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05g}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

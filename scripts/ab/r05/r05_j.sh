@@ -2,7 +2,7 @@
 # Round-5 batch J: the GPU suite with the suspendable sphere walk of the mixed kernel (k_trace_split_tris<MIXED, BVH, 3>),
 # then same-box A/Bs against lib/libhrt_ss0.so (HRT_SPHERE_SUSPEND=0: run to completion in the begin phase) on C5 at
 # 256 spp and the full C5 / C4 bench, and the begin-walk lanes of the new form (diagnostic build).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05j}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

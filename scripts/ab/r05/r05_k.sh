@@ -4,7 +4,7 @@
 # splits; lib/libhrt_ss0.so (HRT_SPHERE_SUSPEND=0, the sphere walk run to completion) against the product on C5
 # (256 spp and the bench line) and C4; suspend_below 16 / 32 on C5; then the diagnostic build's wave records of 1/8
 # C4 and C2 shares and the begin-walk lanes on C5.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05k}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

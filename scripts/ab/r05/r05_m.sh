@@ -2,7 +2,7 @@
 # Round-5 batch M: the GPU suite with cost order auto (a row partition's shares without stealing), then same-box
 # A/Bs of --cost-order 1 against the default on C3 / C2 / C5 (8-way emulated splits; full images are unordered in both),
 # and the diagnostic build's wave records of 1/8 C2 shares with jobs per wave and the last job's time (k_trace).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05m}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

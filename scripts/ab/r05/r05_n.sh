@@ -2,7 +2,7 @@
 # Round-5 batch N: the GPU suite with k_trace_steal (frame-block stealing for the linear sphere scan), then same-box
 # A/Bs on C2: stealing auto (on for its 1/8 shares) against --steal 1, with the 8-way emulated split, and C3 / C5 checks
 # of the final defaults; the diagnostic build's wave records of 1/8 C2 shares.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05n}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

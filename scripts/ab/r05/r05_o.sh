@@ -2,7 +2,7 @@
 # Round-5 batch O: the GPU suite, then same-box A/Bs of stealing on C2 shares (k_trace_steal; auto against --steal 1,
 # with / without the cost order) and on full images (--steal 2 against auto: C2, C3, C4); the diagnostic build's wave
 # records of 1/8 C2 shares with and without stealing.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05o}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

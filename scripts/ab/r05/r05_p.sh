@@ -2,7 +2,7 @@
 # Round-5 batch P: the GPU suite, then same-box A/Bs of the owner's claim size for jobs dealt early (STEAL_OWN_EARLY 4,
 # the product, against lib/libhrt_oe1.so = 1 frame per claim as before): C4 with its 8-way emulated split (stealing
 # auto), and full images with stealing forced on (--steal 2: the claims' cost) for C4 and C3.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05p}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

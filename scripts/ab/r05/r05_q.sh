@@ -2,7 +2,7 @@
 # Round-5 batch Q: the GPU suite with per-XCD job queues (sample buffer), then same-box A/Bs against
 # lib/libhrt_nq0.so (HRT_NQ=0: one job counter for the GPU): C2 (16- and 8-frame jobs), C3, C4 and C5 (256 spp),
 # with the 8-way emulated splits where they run by default.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05q}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

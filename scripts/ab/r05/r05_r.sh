@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 batch R (per-XCD job queues): job sizes for short launches — C2 with 4 / 8 / 16-frame jobs, C3 and C4 with
 # 16 / 32-frame jobs, each with its 8-way emulated split (the knob applies to the full image and every share).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05r}"
 mkdir -p "gpurun_out/$tag"
 for round in 1 2; do

@@ -2,7 +2,7 @@
 # Round-5 batch T: the GPU suite with the cost order's head sorted by cost class, then C4 8-way splits under stealing
 # (the default) against cost order without stealing (32- and 16-frame jobs), C3 and C2 (8-frame jobs) for reference,
 # and the wave records of C4's 1/8 shares 4 / 0 / 5 without stealing.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05t}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

@@ -2,7 +2,7 @@
 # Round-5 diagnosis of short launches and of C3's walk lanes (diagnostic build lib/libhrt_diag.so): per-wave records of a
 # 1/8 C4 share and the full image (scripts/wave_tail.py), the walk's lane counters on C3 (scripts/diag_split.py), and the
 # C2 8-way emulated split by job size. Logs: gpurun_out/<tag>/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05b}"
 mkdir -p "gpurun_out/$tag"
 HRT_LIB=lib/libhrt_diag.so bash scripts/gpu_step.sh "$tag/wave_tail_c4" 300 python scripts/wave_tail.py --config c4 --ranks 8 --rank 4 0 7 --full \

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 batch U (and Z): the GPU suite with the short-launch policy (half-size jobs, cost order instead of stealing for a
 # row partition's shares), then the default bench lines of C4 / C3 / C2 / C5 with their 8-way emulated splits, twice.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05u}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

@@ -2,7 +2,7 @@
 # Round-5 batch X: the GPU parity suite on the final tree, a two-rank gloo rehearsal of the multi-rank line on one GPU
 # (C3 + the C5 leg, gathered image verified bit for bit; both ranks learn their costs in the warmup), and the default
 # bench line.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05x}"
 mkdir -p "gpurun_out/$tag"
 bash scripts/gpu_step.sh "$tag/tests" 900 python -u -m pytest tests/test_gpu_timed.py tests/test_gpu_kernels.py \

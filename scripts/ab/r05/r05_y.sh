@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 batch Y: full images in cost order (--cost-order 2: the costly half of the tiles first, sorted; learnt in the
 # warmup) against raster order (--cost-order 1, the full-image default), C3 / C4 / C2 / C5 (256 spp), same box, 2 rounds.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 tag="${1:-r05y}"
 mkdir -p "gpurun_out/$tag"
 for round in 1 2; do
