@@ -1932,8 +1932,9 @@ struct BlockQueue {
     f3 pr_o = {0.0f, 0.0f, 0.0f}, pr_d = {0.0f, 0.0f, 0.0f};
     uint32_t pr_s = 0, pr_ok = 0;  // this lane's pixel's primary ray for the block, and whether it exists
 #ifdef HRT_STAMPS
-    uint32_t njobs = 0;                // (diagnostic build: jobs this wave took, and when it took its last one)
-    unsigned long long last_job = 0;
+    uint32_t njobs = 0;                // (diagnostic build: jobs this wave took, when it took its last one, and
+    unsigned long long last_job = 0;   // the longest time between two of its job fetches)
+    unsigned long long max_job = 0;
 #endif
 };
 
@@ -1953,8 +1954,12 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
                 if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
 #ifdef HRT_STAMPS
-                B.njobs++;
-                B.last_job = hrt_realtime();
+                {
+                    const unsigned long long now = hrt_realtime();
+                    if (B.njobs) B.max_job = max(B.max_job, now - B.last_job);
+                    B.njobs++;
+                    B.last_job = now;
+                }
 #endif
             }
             B.blk_next = 0;
@@ -2171,7 +2176,9 @@ struct WaveRecord {
     }
     // last_job (k_trace): when the wave took its last job (s_memrealtime; 0: not recorded), as ticks from its start in
     // bits 40-63 of word 2
-    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks, unsigned long long last_job = 0) {
+    // max_job (k_trace): the longest time between two job fetches, in bits 0-23 of word 2 (the HW_ID then dropped)
+    __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks, unsigned long long last_job = 0,
+                           unsigned long long max_job = 0) {
         if (lane != 0u || P.wave_trace == nullptr) return;
         const unsigned long long end = hrt_realtime();
         unsigned hw, xcc;
@@ -2182,7 +2189,8 @@ struct WaveRecord {
         rec[0] = start;
         rec[1] = end;
         const unsigned long long lj = last_job ? min(last_job - start, 0xFFFFFFull) : 0ull;
-        rec[2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) | (lj << 40);
+        const unsigned long long w0 = last_job ? min(max_job, 0xFFFFFFull) : (unsigned long long)hw;
+        rec[2] = w0 | ((unsigned long long)(xcc & 0xFFu) << 32) | (lj << 40);
         rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
     }
 };
@@ -2330,7 +2338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         job_account(J, fin, fl, lane);
     }
 #ifdef HRT_STAMPS
-    wrec.finish(P, lane, BQ.njobs, BQ.last_job);
+    wrec.finish(P, lane, BQ.njobs, BQ.last_job, BQ.max_job);
     {
         // per-lane sums (a lane accrues a region only while it holds a sample): lane-cycles per region;
         // the remainder of the lifetime x 64 is lane-cycles without a sample (refill waits, drain tail)

@@ -53,6 +53,8 @@ def summarise(tr: np.ndarray) -> dict:
         "blocks_per_wave_pcts": pct(blocks),  # (k_trace: jobs per wave)
         "last_job_ms_pcts": pct((st + last_job - t0) / 1e5) if last_job.any() else None,
         "last_job_to_end_ms_pcts": pct((en - st - last_job) / 1e5) if last_job.any() else None,
+        # k_trace: the longest time between two of the wave's job fetches (its longest job but the last)
+        "max_job_ms_pcts": pct((tr[ok, 2].astype(np.int64) & 0xFFFFFF) / 1e5) if last_job.any() else None,
         "blocks_total": int(blocks.sum()),
         "resident_waves_timeline": conc,
     }
