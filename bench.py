@@ -285,6 +285,10 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
 
 
 MODE_NAMES = {0: "sphere", 1: "tris", 2: "mixed"}
+# Rows per block of the multi-GPU row partition: whole 8-row tile rows, except C4, whose Suzanne rows
+# spread more evenly over the ranks in 4-row blocks (8-way emulated split 0.83 -> 0.857; C3 prefers 8: 0.957 against
+# 0.950 with 4; profiles/r05/rb/)
+ROW_BLOCK = {"c4": 4}
 # the frame protocol of every timed step (the reference's golden tests: time 1000 + 10 i, rendering_tests.rs:14-28)
 TIME0, DTIME = 1000, 10
 
@@ -496,9 +500,9 @@ def main() -> int:
     ap.add_argument("--no-golden", action="store_true", help="skip the golden-image check (rank 0, after timing)")
     ap.add_argument("--cpu-rows", type=int, default=108)
     ap.add_argument("--cpu-frames", type=int, default=128)
-    ap.add_argument("--row-block", type=int, default=8,
+    ap.add_argument("--row-block", type=int, default=None,
                     help="multi-GPU split: rows per block dealt round-robin (8 = whole 8x8 tile rows; 1 = single "
-                         "interleaved rows)")
+                         "interleaved rows); default ROW_BLOCK's per-workload choice")
     ap.add_argument("--emulate-ranks", type=int, default=None,
                     help="single-GPU proxy of the N-rank split: render every rank's share here in turn after the "
                          "timed region (default 8 on a one-rank run, 0 = off)")
@@ -510,6 +514,8 @@ def main() -> int:
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU-only rehearsal of the multi-rank path (self-launch, gloo, row-tile gather): no GPU")
     args = ap.parse_args()
+    if args.row_block is None:
+        args.row_block = ROW_BLOCK.get(args.config, 8)
 
     from hrt.launch import needs_self_launch, spawn_ranks
 
