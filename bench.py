@@ -679,6 +679,8 @@ def main() -> int:
                 "fold_bytes": int(st_last.fold_bytes) if schedule == 2 else 0,
                 # frames per trace launch (the sample buffer's balanced launches, rt_params.queue_budget_mb)
                 "launch_frames": int(st_last.launch_frames) if schedule == 2 else 0,
+                # trace launches of the last timed step that dealt their tiles in learnt cost order (rt_params.cost_order)
+                "ordered_launches": int(st_last.ordered_launches) if schedule == 2 else 0,
             },
             # The path is FP32-VALU issue bound (no MFMA: no dense contraction; HBM ~2 % busy). `achieved` =
             # the FP32 FLOPs the kernel executes (its exact in-kernel test counters x FLOP per test, + the
