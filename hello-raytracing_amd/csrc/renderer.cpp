@@ -177,6 +177,7 @@ struct rt_renderer {
     DevBuf<uint4> tb_hnodes;
     DevBuf<uint32_t> tb_order;
     DevBuf<unsigned long long> counter;
+    DevBuf<unsigned long long> count_spread;  // the work counters' CSPREAD copies (rt_kernels.hip flush_counts)
     DevBuf<unsigned long long> steal_slots;  // sample queue: one word per resident wave (frame-block work stealing)
     DevBuf<unsigned long long> queues;       // sample buffer: the per-XCD job counters (rt_kernels.hip queue_take_lane0)
     uint32_t cus = 0;                        // compute units of the renderer's device
@@ -218,7 +219,7 @@ struct rt_renderer {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
                tri_geo.bytes() + mats.bytes() +
-               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + count_spread.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes() + queues.bytes() + tile_cost.bytes() + tile_sum.bytes() + tile_order.bytes() +
                order_scratch.bytes();
     }
@@ -467,8 +468,11 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     }
     // RT_RAW_COUNTERS exported words, then the sample queue's fold-ring watchdog (rt_kernels.hip idle_spin)
     int rc = ensure(r->counter, hrt_dev::COUNTER_WORDS);
+    if (!rc) rc = ensure(r->count_spread, (size_t)hrt_dev::CSPREAD * hrt_dev::CSTRIDE);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(r->counter.ptr, 0, hrt_dev::COUNTER_WORDS * sizeof(unsigned long long), r->stream));
+    HIP_TRY(hipMemsetAsync(r->count_spread.ptr, 0, (size_t)hrt_dev::CSPREAD * hrt_dev::CSTRIDE * sizeof(unsigned long long),
+                           r->stream));
 
     hrt_dev::KParams P{};
     {
@@ -530,6 +534,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     }
     P.mats = r->mats.ptr;
     P.counter = r->counter.ptr;
+    P.count_spread = r->count_spread.ptr;
 #ifdef HRT_STAMPS
     {
         // k_render's waves, or the persistent kernels' (at most steal_cap = 32 per CU)
@@ -857,6 +862,12 @@ int finish_stats(rt_renderer* r) {
     unsigned long long* q = r->raw_counters;
     unsigned long long wd[4] = {};
     HIP_TRY(hipMemcpy(q, r->counter.ptr, RT_RAW_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    {  // the work counters' copies (rt_kernels.hip flush_counts) into words 0-4
+        std::vector<unsigned long long> sp((size_t)hrt_dev::CSPREAD * hrt_dev::CSTRIDE);
+        HIP_TRY(hipMemcpy(sp.data(), r->count_spread.ptr, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < hrt_dev::CSPREAD; k++)
+            for (uint32_t c = 0; c < 5u; c++) q[c] += sp[(size_t)k * hrt_dev::CSTRIDE + c];
+    }
     HIP_TRY(hipMemcpy(wd, r->counter.ptr + hrt_dev::WATCHDOG, sizeof wd, hipMemcpyDeviceToHost));
     if (wd[0] || wd[3]) {  // waves gave up waiting for a fold-ring slot: the image is incomplete; report, do not hang
         // diagnostic build: HRT_RING_DUMP=path writes the fold-ring control words (tile done masks, tile locks and
@@ -926,6 +937,7 @@ void delete_buffers(rt_renderer* r) {
     r->tb_hnodes.release();
     r->tb_order.release();
     r->counter.release();
+    r->count_spread.release();
     r->steal_slots.release();
     r->queues.release();
     r->samples.release();

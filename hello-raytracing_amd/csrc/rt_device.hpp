@@ -80,6 +80,12 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 // device counter words: [0, 16) exported (include/hrt.h RT_RAW_COUNTERS; [15] = the job queue), then the
 // fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue overruns
 constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
+// the five work counters (queries, box / sphere tests, node / triangle tests) as CSPREAD copies, CSTRIDE words apart:
+// a wave adds its sums to copy (wave id % CSPREAD), the host adds the copies (renderer.cpp finish_stats)
+#ifndef HRT_CSPREAD
+#define HRT_CSPREAD 64
+#endif
+constexpr uint32_t CSPREAD = HRT_CSPREAD, CSTRIDE = 16;
 
 // fold ring: jobs per tile and launch (the done bits of a tile's fold word, rt_kernels.hip)
 constexpr uint32_t FOLD_MAX_JOBS = 48;
@@ -184,6 +190,7 @@ struct KParams {
     // tiles in descending order of their last learnt cost (rt_kernels.hip k_order_*)
     uint32_t* tile_cost;
     const uint32_t* tile_order;
+    unsigned long long* count_spread;  // CSPREAD x CSTRIDE words: the work counters' copies
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

@@ -165,6 +165,18 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
     return bi;
 }
 
+// Lane 0 of a wave, at its end: its work counts (queries, box / sphere tests, node / triangle tests) added to its copy of
+// the counters (wave id % CSPREAD). One set of counters for every wave made the launch's last ~1 ms a queue of
+// same-address atomics (C2: 6144 waves x 5).
+__device__ __forceinline__ void flush_counts(const unsigned long long (&sums)[5]) {
+    const KPtr K = kargs();
+    const uint32_t wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    unsigned long long* const c = K->count_spread + (wid % CSPREAD) * CSTRIDE;
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        if (sums[k]) atomicAdd(c + k, sums[k]);
+}
+
 struct Tally {
     uint32_t boxes = 0, spheres = 0;  // sphere culling BVH box tests, ray-sphere tests
     uint32_t nodes = 0, tris = 0;     // triangle program: implicit-heap node tests, triangle tests
@@ -2141,11 +2153,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
-    if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
-    }
+    if (lane == 0) flush_counts(sums);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2371,11 +2379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
-    if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(P.counter + c, sums[c]);
-    }
+    if (lane == 0) flush_counts(sums);
 }
 
 
@@ -2756,12 +2760,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
-    if (lane == 0) {
-        unsigned long long* const cnt = kargs()->counter;  // (loaded here, not held in SGPRs)
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(cnt + c, sums[c]);
-    }
+    if (lane == 0) flush_counts(sums);
 }
 
 // Sample queue with suspendable walks for the triangle and mixed programs (reference heap walk; the
@@ -2954,12 +2953,7 @@ k_trace_split_tris(const KParams P) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sums[c] += __shfl_xor(sums[c], off);
     }
-    if (lane == 0) {
-        unsigned long long* const cnt = kargs()->counter;  // (loaded here, not held in SGPRs across the kernel)
-#pragma unroll
-        for (int c = 0; c < 5; c++)
-            if (sums[c]) atomicAdd(cnt + c, sums[c]);
-    }
+    if (lane == 0) flush_counts(sums);
 }
 
 // Sample buffer (ring_mode 0): folds P.nframes sample colours per pixel into the image, in frame order, with the
