@@ -81,7 +81,7 @@ constexpr int BVH_STACK = HRT_BVH_STACK;  // traversal stack entries per lane (L
 // fold-ring watchdog: fires, the last firing wave's waiting job and its entry flags, free-queue overruns
 constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
 // the five work counters (queries, box / sphere tests, node / triangle tests) as CSPREAD copies, CSTRIDE words apart:
-// a wave adds its sums to copy (wave id % CSPREAD), the host adds the copies (renderer.cpp finish_stats)
+// a wave adds its sums to one copy (rt_kernels.hip flush_counts; CSPREAD a power of two), the host adds the copies
 #ifndef HRT_CSPREAD
 #define HRT_CSPREAD 64
 #endif

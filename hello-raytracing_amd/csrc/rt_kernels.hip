@@ -169,12 +169,14 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
 // the counters (wave id % CSPREAD). One set of counters for every wave made the launch's last ~1 ms a queue of
 // same-address atomics (C2: 6144 waves x 5).
 __device__ __forceinline__ void flush_counts(const unsigned long long (&sums)[5]) {
-    const KPtr K = kargs();
-    const uint32_t wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    unsigned long long* const c = K->count_spread + (wid % CSPREAD) * CSTRIDE;
+    // (any spread of the waves over the copies will do: the wave's hardware slot — wave, SIMD, CU, shader engine in
+    // HW_ID, a scalar read here — and its workgroup; threadIdx-based indices kept a VGPR alive across the kernel)
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t idx = (hw ^ (hw >> 8) ^ (hw >> 13) ^ blockIdx.x) & (CSPREAD - 1u);
+    unsigned long long* const c = kargs()->count_spread + idx * CSTRIDE;
 #pragma unroll
-    for (int k = 0; k < 5; k++)
-        if (sums[k]) atomicAdd(c + k, sums[k]);
+    for (int k = 0; k < 5; k++) atomicAdd(c + k, sums[k]);
 }
 
 struct Tally {
