@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-5 batch RB: row-block size of the row partition (8 = default: whole 8-row tile rows dealt round-robin; 1 = single
 # interleaved rows; 2 / 4) on the 8-way emulated splits of C2 / C4 / C3 (the full image is the same in each).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag="${1:-r05rb}"
 mkdir -p "gpurun_out/$tag"
 for round in 1 2; do
