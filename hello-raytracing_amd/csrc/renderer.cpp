@@ -731,7 +731,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 #ifndef HRT_NQ
 #define HRT_NQ 1
 #endif
-        constexpr size_t QWORDS = 8u * 16u + 16u;  // NQ x QSTRIDE, then the dry-queue mask (its own line)
+        constexpr size_t QWORDS = 8u * 16u;  // NQ x QSTRIDE
         P.queues = nullptr;
         if (HRT_NQ && !P.ring_mode) {
             rc = ensure(r->queues, QWORDS);

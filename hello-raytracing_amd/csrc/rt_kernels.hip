@@ -1640,9 +1640,6 @@ __device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uin
 // its XCD's queue first, then from the others in turn (the queues it found exhausted kept in its WJ_QDEAD word: the
 // ring's slot words, unused with the sample buffer). With one counter for the whole GPU every job fetch is an atomic
 // on one address from every XCD. Lane 0; returns >= njobs when every queue is exhausted.
-#ifndef HRT_QMASK
-#define HRT_QMASK 1
-#endif
 constexpr uint32_t NQ = 8, QSTRIDE = 16, WJ_QDEAD = WJ_SLOT;
 __device__ __forceinline__ uint32_t queue_take_lane0(const WaveJobs& J, const KPtr K) {
     unsigned long long* const qs = K->queues;
@@ -1650,12 +1647,6 @@ __device__ __forceinline__ uint32_t queue_take_lane0(const WaveJobs& J, const KP
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
     uint32_t dead = J.w[WJ_QDEAD], j = 0xFFFFFFFFu;
-#if HRT_QMASK
-    // Once its own queue is dry a wave skips the queues some wave already found dry (bit q of the word after the
-    // queues, set by the wave that found it): the fetches of every wave from every dry queue queued at the launch's end.
-    unsigned int* const qmask = (unsigned int*)(qs + NQ * QSTRIDE);
-    if ((dead >> (x & (NQ - 1u))) & 1u) dead |= __hip_atomic_load(qmask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     for (uint32_t i = 0; i < NQ; i++) {
         const uint32_t q = (x + i) & (NQ - 1u);
         if ((dead >> q) & 1u) continue;
@@ -1665,9 +1656,6 @@ __device__ __forceinline__ uint32_t queue_take_lane0(const WaveJobs& J, const KP
             break;
         }
         dead |= 1u << q;
-#if HRT_QMASK
-        atomicOr(qmask, 1u << q);
-#endif
     }
     J.w[WJ_QDEAD] = dead;
     return j;
