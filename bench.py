@@ -489,6 +489,8 @@ def main() -> int:
     ap.add_argument("--cost-order", type=int, default=None,
                     help="sample queue: 0 auto (the most expensive tiles first for a row partition's shares "
                          "without stealing), 1 off, 2 on")
+    ap.add_argument("--packet", type=int, default=None,
+                    help="sphere program: primary rays walked as one packet per frame block: 0 auto (on), 1 off, 2 on")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,
@@ -573,6 +575,8 @@ def main() -> int:
         extra["tail_split"] = args.tail_split
     if args.cost_order is not None:
         extra["cost_order"] = args.cost_order
+    if args.packet is not None:
+        extra["packet"] = args.packet
     # the timed draws run the default kernels (count_tests 0: the sphere program's k_trace_split does not count its box
     # and sphere tests); the warmup draws count them (count_tests 1) for the per-ray figures of the line, the same
     # every step (bit-identical draws)

@@ -562,6 +562,8 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     P.bvh_rr_h = std::nextafter(B.root_radius * (1.0f + 0x1p-9f), INFINITY);
     P.bvh_nnodes = (uint32_t)B.nodes.size();
     P.bvh_lnodes = (HRT_LNODES && B.nodes.size() <= hrt_dev::LNODE_CAP && B.depth <= hrt_dev::LNODE_DEPTH) ? 1u : 0u;
+    // (0 auto = off: the packet walk measured -8 % on C3)
+    P.packet = (P.bvh_lnodes && r->params.packet == 2u) ? 1u : 0u;
     // delta = 8u r_max + min(16u D^2 / r_min, 2e-3 D) + 4u D + 4e-23/|d|  (u = 2^-24)
     const float u = 0x1p-24f;
     P.pad_k1 = 8.0f * u * B.r_max;
@@ -1036,6 +1038,13 @@ int rt_destroy(rt_renderer* r) {
     return RT_OK;
 }
 
+int rt_abi_version(uint32_t* version, uint32_t* params_bytes, uint32_t* stats_bytes) {
+    if (version) *version = RT_ABI_VERSION;
+    if (params_bytes) *params_bytes = (uint32_t)sizeof(rt_params);
+    if (stats_bytes) *stats_bytes = (uint32_t)sizeof(rt_stats);
+    return RT_OK;
+}
+
 int rt_get_params(const rt_renderer* r, rt_params* out) {
     if (!r || !out) return fail(RT_ERR_ARG, "rt_get_params: null");
     *out = r->params;
@@ -1061,6 +1070,7 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
     if (p->count_tests > 1) return fail(RT_ERR_ARG, "rt_set_params: count_tests must be 0 or 1");
+    if (p->packet > 2) return fail(RT_ERR_ARG, "rt_set_params: packet must be 0 auto, 1 off or 2 on");
     if (p->cost_order > 3)
         return fail(RT_ERR_ARG, "rt_set_params: cost_order must be 0 auto, 1 off, 2 on or 3 on, learning in every launch");
     const bool rows_changed = p->row0 != r->params.row0 || p->row_step != r->params.row_step ||

@@ -135,7 +135,8 @@ struct KParams {
                                   // renderer.cpp pack_bvh_hnodes); bvh_nodes is the f32 form (bvh_run<.., false>)
     float bvh_rr_h;               // radius bound of the fp16 boxes (>= their half-diagonal)
     uint32_t bvh_nnodes;          // nodes in bvh_hnodes
-    uint32_t bvh_lnodes, pad_ln;  // 1: k_trace_split keeps the nodes in LDS (<= LNODE_CAP nodes, depth <= 8)
+    uint32_t bvh_lnodes;          // 1: k_trace_split keeps the nodes in LDS (<= LNODE_CAP nodes, depth <= 8)
+    uint32_t packet;              // 1 (with bvh_lnodes): k_trace_split<.., PACKET> walks primary rays as packets
     float pad_k1, pad_k2, pad_k3, pad_k4;  // per-query padding constants (DESIGN.md §Sphere BVH)
     // opt-in SAH triangle tree (rt_params.tri_bvh; host/tri_bvh.hpp), nodes with fp16 boxes like bvh_hnodes
     const uint32_t* tb_order;     // triangle index of each leaf entry

@@ -695,13 +695,14 @@ __device__ __forceinline__ float div_by_radius(float x, float radius, float inv_
     return x / radius;
 }
 
-__device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
+// The hit record from the hit point p = point_on_ray(o, d, t) (k_trace_split's packet-resolved primary rays carry p
+// instead of the origin; h.t is not read after the record is made)
+__device__ __forceinline__ void sphere_record_p(const KParams& P, const f3 p, const f3 d, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
-    const f3 p = point_on_ray(r.o, r.d, t);
     f3 n = p - mk(s.cx, s.cy, s.cz);
     n = mk(div_by_radius(n.x, s.radius, s.inv_radius), div_by_radius(n.y, s.radius, s.inv_radius),
            div_by_radius(n.z, s.radius, s.inv_radius));
-    const bool front = dot(r.d, n) < 0.0f;
+    const bool front = dot(d, n) < 0.0f;
     if (!front) n = -n;
     h.p = p;
     h.n = n;
@@ -709,6 +710,91 @@ __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, in
     h.ar = s.ar; h.ag = s.ag; h.ab = s.ab; h.param = s.param;
     h.id = ((uint32_t)bi << 3) | 4u | (s.id == 1u || s.id == 2u ? s.id : 0u);
     h.front = front;
+}
+__device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
+    sphere_record_p(P, point_on_ray(r.o, r.d, t), r.d, bi, t, h);
+}
+
+// Coherent primary rays walked as one packet (k_trace_split<.., PACKET>). The 64 primary rays of
+// a frame block (one frame of one 8x8 tile) are nearly parallel: the union of the nodes their own walks visit is
+// barely larger than one walk (C3 model, scripts/studies/packet_sim.cpp: 7.7 node steps per block for 7.4 per ray).
+// The calling lanes (those whose query needs the walk, bvh_begin true) walk that union together: every decision is
+// wave-uniform — a child is visited when any lane's padded box test passes, the near child first by the lanes' vote —
+// so each step runs with every lane, the node words come from LDS at one address, and the stack is one VGPR (lane k
+// holds the k-th pending node; depth <= LNODE_DEPTH). Every lane tests every sphere of a visited leaf with the
+// reference arithmetic and keeps the (t, slot) lexicographic minimum, which does not depend on the visiting order.
+// Exact for the same reason bvh_run is: a lane's best t never drops below its winner's t, so the lane's own padded
+// test passes every box on the path to its winner's leaf, the packet visits that leaf, and the lane tests the winner;
+// the spheres the packet adds are real candidates and cannot displace it. Same bits and query count as bvh_run.
+template <bool COUNT>
+__device__ __forceinline__ bool packet_walk(const KParams& P, const float4* __restrict__ e, BvhQuery& Q,
+                                            const uint4* __restrict__ hn, Tally& tally, bool part) {
+    // Called by all 64 lanes (the wave-uniform stack lives in one VGPR whose lane k every lane must be able to write);
+    // `part`: the lane's ray takes part — a lane outside the image or with an uncovered ray enters with best t = -1,
+    // so no box or sphere test of it passes and it never votes. The participants' direction signs must agree (C3:
+    // all but the tiles a coordinate plane of the direction crosses): the sign-ordered test's pair rotations are then
+    // wave-uniform (SGPRs). Else the rays stay unresolved and walk on their own (qs 0).
+    const Slab S = Q.S;
+    const uint32_t nx = __float_as_uint(S.inv.x) >> 31, ny = __float_as_uint(S.inv.y) >> 31,
+                   nz = __float_as_uint(S.inv.z) >> 31;
+    if (__ballot(1) != ~0ull) return false;  // (every lane must be active: see above)
+    const unsigned long long act = __ballot(part);
+    const unsigned long long bx = __ballot(part && nx != 0u), by = __ballot(part && ny != 0u), bz = __ballot(part && nz != 0u);
+    if (act == 0ull || (bx != 0ull && bx != act) || (by != 0ull && by != act) || (bz != 0ull && bz != act)) return false;
+    const uint32_t shx = bx ? 16u : 0u, shy = by ? 16u : 0u, shz = bz ? 16u : 0u;
+    float bt = Q.bt;
+    int bc = Q.bc;
+    uint32_t node = P.bvh_root;  // wave-uniform (SGPRs): the walk's node, stack depth and child words
+    uint32_t stk = 0u, sp = 0u;  // the stack: lane k holds the k-th pending node
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+    while (true) {
+        if (!(node & BVH_LEAF_BIT)) {
+            float tl, tr;
+            const uint4 c0 = hn[2 * node], c1 = hn[2 * node + 1];
+            const bool hl = box_hit_so(c0.x, c0.y, c0.z, shx, shy, shz, S, bt, tl);
+            const bool hr = box_hit_so(c1.x, c1.y, c1.z, shx, shy, shz, S, bt, tr);
+            const uint32_t left = __builtin_amdgcn_readfirstlane(c0.w), right = __builtin_amdgcn_readfirstlane(c1.w);
+            if constexpr (COUNT) tally.boxes += part ? 2u : 0u;
+            const unsigned long long ml = __ballot(hl), mr = __ballot(hr);
+            if ((ml | mr) != 0ull) {
+                if (ml != 0ull && mr != 0ull) {
+                    // the near child of most lanes first (lanes that enter one child only vote for it)
+                    const unsigned long long vl = __ballot(hl && (!hr || tl <= tr));
+                    const bool lf = 2u * (uint32_t)__popcll(vl) >= (uint32_t)__popcll(ml | mr);
+                    stk = __lane_id() == sp ? (lf ? right : left) : stk;  // (no v_writelane builtin here)
+                    sp++;
+                    node = lf ? left : right;
+                } else {
+                    node = ml != 0ull ? left : right;
+                }
+                continue;
+            }
+        } else {
+            // the ray from the lane's block entry (not held in registers through the walk)
+            const float4 e0 = e[0], e1 = e[1];
+            const Ray r = {mk(e0.x, e0.y, e0.z), mk(e0.w, e1.x, e1.y)};
+            const float a = dot(r.d, r.d);
+            const float a4 = 4.0f * a, a2 = 2.0f * a;
+            const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+            for (uint32_t o = first * 16u, oe = (first + cnt) * 16u; o != oe; o += 16u) {
+                const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
+                const float t = exact_t_geo<true>(float4{v.x, v.y, v.z, v.w}, r, a4, a2);
+                if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
+                    const int slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)(o >> 2), 0, 0);
+                    if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(o >> 4); }
+                }
+            }
+            if constexpr (COUNT) tally.spheres += part ? cnt : 0u;
+        }
+        if (sp == 0u) break;
+        sp--;
+        node = __builtin_amdgcn_readlane(stk, sp);
+    }
+    Q.bt = bt;
+    Q.bc = bc;
+    return true;
 }
 
 // intersect_node (shader_tris.wgsl:150-159); inv = 1/d is the same value for every node of a query.
@@ -2555,8 +2641,22 @@ __device__ __forceinline__ void refill_block_lds(const KParams& P, BlockState& B
 // workgroup and the stack shrinks to 8 entries (a path holds at most depth pending siblings), 22 KB in all.
 // STEAL: frame-block work stealing (sample buffer; renderer.cpp turns it on for launches with few jobs per wave).
 // A separate instantiation: the runtime-switched form cost C3 3 % with stealing off (register allocation).
-template <bool LNODES, bool STEAL, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_trace_split(const KParams P) {
+// PACKET (with LNODES; rt_params.packet): each frame block's primary rays are walked as one packet when the block is
+// made (packet_walk: all 64 lanes, wave-uniform traversal), and the block entry carries the resolved first hit — the
+// hit point in place of the origin and the winner's slot — so a lane that takes the sample shades it at once (qs 4)
+// instead of walking its primary ray beside the wave's incoherent secondary walks. Same bits and query counts.
+template <bool LNODES, bool STEAL, bool COUNT, bool PACKET>
+#ifndef HRT_PACKET_WAVES
+#define HRT_PACKET_WAVES 7
+#endif
+#ifndef HRT_PACKET_STEAL_WAVES
+#define HRT_PACKET_STEAL_WAVES 6  // (the stealing packet kernel spills 6 VGPRs at 7 waves)
+#endif
+#ifndef HRT_SPLIT_WAVES
+#define HRT_SPLIT_WAVES 7
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (STEAL ? HRT_PACKET_STEAL_WAVES : HRT_PACKET_WAVES) : HRT_SPLIT_WAVES))) void k_trace_split(const KParams P) {
+    static_assert(!PACKET || LNODES, "the packet walk reads the LDS nodes and keeps its stack in one VGPR (depth <= 8)");
     constexpr int MODE = MODE_SPHERE;
     constexpr int SPLIT_STACK = LNODES ? (int)LNODE_DEPTH : 14;
     const uint32_t lane = threadIdx.x & 63u;
@@ -2571,7 +2671,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
     bool drained = false;
@@ -2630,19 +2729,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                 const uint32_t pok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
                 Ray pr = {mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
                 uint32_t ps = 0;
+                uint32_t ew = pok;  // entry word: bit 0 in the image, PACKET: bit 1 resolved, bit 2 hit, slot << 3
                 if (pok) {
                     const KPtr K = kargs();  // row map and time: loaded here, not held in SGPRs
                     const uint32_t y = global_row(K->row0, K->row_block, K->row_stride, kr);
                     pr = primary_ray<MODE>(&K->cam, x, y, K->time0 + (job_f0 + blk_f) * K->dtime, ps);
                 }
                 blk[2 * threadIdx.x] = float4{pr.o.x, pr.o.y, pr.o.z, pr.d.x};
-                blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(pok)};
+                blk[2 * threadIdx.x + 1] = float4{pr.d.y, pr.d.z, __uint_as_float(ps), __uint_as_float(ew)};
+                if constexpr (PACKET) {
+                    // (bounce cap 0: no query; rays bvh_begin leaves to the full scan: resolved later, qs 0)
+#ifndef HRT_PACKET_DRY
+#define HRT_PACKET_DRY 0  // (A/B builds only: 1 = the packet kernel without its walk, every primary ray unresolved)
+#endif
+                    if (P.bounces > 0u && !HRT_PACKET_DRY) {  // (wave-uniform: every lane enters the packet walk)
+                        BvhQuery Qp;
+                        // slab constants only (bvh_begin's uncovered-ray rule); the large list after the walk: the
+                        // (t, slot) minimum does not depend on the order, and the walk then holds fewer registers
+                        const float a2 = 2.0f * dot(pr.d, pr.d);
+                        const bool cov = pok && (a2 > 0x1p-100f && a2 < 0x1p100f) && __builtin_isfinite(pr.o.x) &&
+                                         __builtin_isfinite(pr.o.y) && __builtin_isfinite(pr.o.z);
+                        Qp.bt = cov ? FLT_MAX_REF : -1.0f;  // (-1: no test passes)
+                        Qp.bc = -1;
+                        bvh_slab<true, true>(P, pr, Qp);
+                        if (packet_walk<COUNT>(P, blk + 2 * threadIdx.x, Qp, lnodes, tally, cov) && cov) {
+                            // the entry: the hit point in place of the origin and the winner's slot, or a resolved miss
+                            // (everything re-read from the entry: nothing of the block kept in registers through the walk)
+                            uint32_t rw = 3u;
+                            const float4 e0 = blk[2 * threadIdx.x], e1 = blk[2 * threadIdx.x + 1];
+                            const Ray re = {mk(e0.x, e0.y, e0.z), mk(e0.w, e1.x, e1.y)};
+                            {
+                                const float a = dot(re.d, re.d);
+                                const uint32_t nlarge = kargs()->nlarge;
+                                for (uint32_t k = 0; k < nlarge; k++) {
+                                    const int i = P.large_slots[k];
+                                    const float t = exact_t_geo<true>(P.sph_geo[i], re, 4.0f * a, 2.0f * a);
+                                    if (beats(t, i, Qp.bt, Qp.bc >= 0 ? bvh_slot_of(P, Qp.bc) : -1)) {
+                                        Qp.bt = t;
+                                        Qp.bc = (int)(P.bvh_nleaf + k);
+                                    }
+                                }
+                                if constexpr (COUNT) tally.spheres += nlarge;
+                            }
+                            if (Qp.bc >= 0) {
+                                const f3 ph = point_on_ray(re.o, re.d, Qp.bt);
+                                blk[2 * threadIdx.x].x = ph.x;
+                                blk[2 * threadIdx.x].y = ph.y;
+                                blk[2 * threadIdx.x].z = ph.z;
+                                rw = 7u | ((uint32_t)bvh_slot_of(P, Qp.bc) << 3);
+                            }
+                            blk[2 * threadIdx.x + 1].w = __uint_as_float(rw);
+                        }
+                    }
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const uint32_t avail = 64u - blk_next;
-            const uint32_t rank = (uint32_t)__popcll(m & below);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             const int src = (int)((blk_next + rank) & 63u);
             const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src)];
             const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src) + 1];
@@ -2651,8 +2796,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             bool took = false;
             if (need && rank < avail) {
                 need = false;
-                if (ok) {
-                    ray.o = mk(ox, oy, oz);
+                if (ok & 1u) {
+                    ray.o = mk(ox, oy, oz);  // (PACKET, resolved hit: the hit point)
                     ray.d = mk(dx, dy, dz);
                     s = ss;
                     fl = sample_ref(J, job_f0, blk_f);
@@ -2662,6 +2807,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                     bounce = 0;
                     have = true;
                     qs = 0;
+                    if constexpr (PACKET) {
+                        if (ok & 2u) {  // resolved by the packet: shade at once, the winner's slot (or -1) in Q.bc
+                            qs = 4u;
+                            Q.bc = (ok & 4u) ? (int)(ok >> 3) : -1;
+                        }
+                    }
                     took = true;
                 }
             }
@@ -2703,19 +2854,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 2u);
+        // (the queries shaded this round, counted per wave: a wave-uniform count needs no VGPR)
+        queries += (uint32_t)__popcll(__ballot(have && (qs == 2u || (PACKET && qs == 4u))));
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
             tally.lshade++;
             if (first_active_lane()) tally.wshade++;
 #endif
             bool done = true;
-            if (qs == 2u) {
+            if (qs == 2u || (PACKET && qs == 4u)) {
                 float best = FLT_MAX_REF;
-                const int bi = bvh_end<true>(P, ray, Q, best, tally);
-                queries++;
+                int bi;
+                f3 p;
+                if (PACKET && qs == 4u) {  // a primary ray the packet resolved: ray.o is its hit point
+                    bi = Q.bc;
+                    p = ray.o;
+                } else {
+                    bi = bvh_end<true>(P, ray, Q, best, tally);
+                    p = point_on_ray(ray.o, ray.d, best);
+                }
                 if (bi >= 0) {
                     Hit h;
-                    sphere_record(P, ray, bi, best, h);
+                    sphere_record_p(P, p, ray.d, bi, best, h);
                     scatter<MODE>(P, s, ray, h);
                     att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                     bounce++;
@@ -2756,7 +2916,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
     if (lane == 0)
         for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
 #endif
-    unsigned long long sums[5] = {queries, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+    unsigned long long sums[5] = {lane == 0u ? queries : 0u, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
 #pragma unroll
@@ -3226,9 +3386,9 @@ hipError_t hrt_check_exact_math(unsigned long long n, uint32_t seed, unsigned lo
 static thread_local char g_kernel_name[64] = "";
 const char* hrt_last_kernel() { return g_kernel_name; }
 void hrt_reset_last_kernel() { g_kernel_name[0] = '\0'; }
-static const char* kname_bbb(const char* base, int a, int b, int c) {  // <bool, bool, bool>
-    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s, %s>", base, a ? "true" : "false", b ? "true" : "false",
-             c ? "true" : "false");
+static const char* kname_bbbb(const char* base, int a, int b, int c, int d) {  // <bool, bool, bool, bool>
+    snprintf(g_kernel_name, sizeof g_kernel_name, "%s<%s, %s, %s, %s>", base, a ? "true" : "false", b ? "true" : "false",
+             c ? "true" : "false", d ? "true" : "false");
     return g_kernel_name;
 }
 static const char* kname_iiib(const char* base, int a, int b, int c, int d) {  // <int, int, int, bool>
@@ -3317,15 +3477,19 @@ static hipError_t launch_trace_mode(int variant, const KParams& P, hipStream_t s
     }
 }
 
-// k_trace_split<LNODES, STEAL, COUNT> by P.bvh_lnodes / P.steal
+// k_trace_split<LNODES, STEAL, COUNT, PACKET> by P.bvh_lnodes / P.steal / P.packet (PACKET only with LNODES)
 template <bool COUNT>
 static hipError_t launch_trace_split(const KParams& P, hipStream_t stream) {
     const char* base = "k_trace_split";
+    if (P.bvh_lnodes && P.packet) {
+        return P.steal ? launch_persistent(k_trace_split<true, true, COUNT, true>, P, stream, kname_bbbb(base, 1, 1, COUNT, 1))
+                       : launch_persistent(k_trace_split<true, false, COUNT, true>, P, stream, kname_bbbb(base, 1, 0, COUNT, 1));
+    }
     if (P.steal)
-        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT>, P, stream, kname_bbb(base, 1, 1, COUNT))
-                            : launch_persistent(k_trace_split<false, true, COUNT>, P, stream, kname_bbb(base, 0, 1, COUNT));
-    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT>, P, stream, kname_bbb(base, 1, 0, COUNT))
-                        : launch_persistent(k_trace_split<false, false, COUNT>, P, stream, kname_bbb(base, 0, 0, COUNT));
+        return P.bvh_lnodes ? launch_persistent(k_trace_split<true, true, COUNT, false>, P, stream, kname_bbbb(base, 1, 1, COUNT, 0))
+                            : launch_persistent(k_trace_split<false, true, COUNT, false>, P, stream, kname_bbbb(base, 0, 1, COUNT, 0));
+    return P.bvh_lnodes ? launch_persistent(k_trace_split<true, false, COUNT, false>, P, stream, kname_bbbb(base, 1, 0, COUNT, 0))
+                        : launch_persistent(k_trace_split<false, false, COUNT, false>, P, stream, kname_bbbb(base, 0, 0, COUNT, 0));
 }
 
 hipError_t hrt_launch_trace(int mode, int variant, const KParams& P, hipStream_t stream) {

@@ -51,6 +51,7 @@ class RtParams(C.Structure):
         ("tail_split", C.c_uint32),
         ("count_tests", C.c_uint32),
         ("cost_order", C.c_uint32),
+        ("packet", C.c_uint32),
     ]
 
 
@@ -112,6 +113,7 @@ SIGNATURES = {
     "rt_get_wave_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_get_device": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_last_error": (C.c_char_p, []),
+    "rt_abi_version": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "rt_device_count": (C.c_int, []),
     "rt_build_info": (C.c_char_p, []),
     "rt_host_check_bvh_sizes": (C.c_int, [_PU32, _U32, _U32, _U32]),
@@ -158,6 +160,40 @@ def _torch_hip_runtime() -> Path | None:
     return p if p.exists() else None
 
 
+def elf_dynamic_names(path: Path | str, tag: int) -> list:
+    """Strings of one dynamic-section tag of a 64-bit little-endian ELF (1 = DT_NEEDED, 14 = DT_SONAME); [] when the
+    file cannot be read as one. Reads the section headers only, loads nothing."""
+    import struct
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return []
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        return []
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    for sh in secs:
+        if sh[1] != 6:  # SHT_DYNAMIC
+            continue
+        strtab = secs[sh[6]]  # sh_link: its string table
+        out = []
+        for off in range(sh[4], sh[4] + sh[5], 16):
+            d_tag, d_val = struct.unpack_from("<qQ", data, off)
+            if d_tag == 0:
+                break
+            if d_tag == tag:
+                a = strtab[4] + d_val
+                out.append(data[a:data.index(b"\0", a)].decode())
+        return out
+    return []
+
+
+# which HIP runtime lib() bound libhrt.so to, and why (read by tests and the bench's device report)
+HIP_RUNTIME_CHOICE = {"path": None, "reason": "not loaded"}
+
+
 def hip_runtimes() -> set:
     """Real paths of the HIP runtime libraries (libamdhip64*) mapped into this process (/proc/self/maps)."""
     out = set()
@@ -198,11 +234,23 @@ def lib() -> C.CDLL:
                 "(or __graft_entry__.build()); the renderer has no Python/CPU fallback"
             )
         trt = _torch_hip_runtime()
-        if trt is not None:
+        needed = [n for n in elf_dynamic_names(LIB_PATH, 1) if n.startswith("libamdhip64")]
+        if trt is None:
+            HIP_RUNTIME_CHOICE.update(path=None, reason="torch not installed: the runtime libhrt.so's RUNPATH finds")
+        elif elf_dynamic_names(trt, 14) == needed and needed:
+            # same SONAME: torch's copy satisfies libhrt.so's DT_NEEDED, so one runtime serves both
             C.CDLL(os.fspath(trt), mode=C.RTLD_GLOBAL)
+            HIP_RUNTIME_CHOICE.update(path=os.fspath(trt), reason=f"torch's runtime preloaded (SONAME {needed[0]})")
+        else:
+            # another ROCm major: preloading would map two runtimes; libhrt.so keeps its own, and a process that also
+            # uses torch's GPU runtime fails check_single_hip_runtime at its first renderer
+            HIP_RUNTIME_CHOICE.update(path=None, reason=f"torch's runtime {elf_dynamic_names(trt, 14)} does not match "
+                                                       f"libhrt.so's {needed}: not preloaded")
         L = C.CDLL(os.fspath(LIB_PATH))
         check_single_hip_runtime()
         for name, (res, args) in {**SIGNATURES, **TESTING_SIGNATURES}.items():
+            if "HRT_LIB" in os.environ and not hasattr(L, name):
+                continue  # (an older library named for an A/B run: the product library must export every symbol)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -125,6 +125,12 @@ typedef struct rt_params {
                                   does not steal once it has learnt, and for the suspendable-walk kernels (not
                                   the linear scans' full images), 1 off, 2 on, 3 on with every launch learning;
                                   bit-identical always                           */
+    uint32_t packet;           /* sphere program, culling BVH with its nodes in LDS (k_trace_split): walk each frame
+                                  block's 64 primary rays as one coherent packet when the block is made (one
+                                  wave-uniform traversal of the union of their nodes) and hand the samples out with
+                                  their first hit resolved: 0 auto = off, 1 off, 2 on; bit-identical images and
+                                  query counts (box / sphere test counts then count the packet's tests). Off by
+                                  default: C3 35.2 vs 38.3 Grays/s                 */
 } rt_params;
 
 #define RT_FOLD_AUTO 0u
@@ -252,6 +258,12 @@ int rt_check_exact_math(uint64_t n, uint32_t seed, uint64_t mismatches[3]);
  * {domain, bus, device}. A process must load ONE HIP runtime for the ordinal to mean what the caller's runtime
  * means (hrt/_lib.py loads the one torch uses). */
 int rt_get_device(const rt_renderer *r, int32_t *ordinal, int32_t pci[3]);
+
+/* ABI guard (no reference counterpart): rt_params and rt_stats grow at their ends between versions, and rt_set_params
+ * / rt_get_stats copy this header's sizes. A caller built against another header checks *version == RT_ABI_VERSION (or
+ * the two sizes against its own sizeof) before the first rt_set_params / rt_get_stats. Any pointer may be NULL. */
+#define RT_ABI_VERSION 6u /* 6: rt_params.packet (round 6); 5: rt_params.cost_order, rt_stats.ordered_launches */
+int rt_abi_version(uint32_t *version, uint32_t *params_bytes, uint32_t *stats_bytes);
 
 /* Thread-local message for the last failing call. */
 const char *rt_last_error(void);

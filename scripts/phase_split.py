@@ -31,13 +31,15 @@ def main() -> None:
     ap.add_argument("--config", default="c5")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--suspend-below", type=int, nargs="+", default=[None])
+    ap.add_argument("--packet", type=int, default=0, help="rt_params.packet (sphere program): 0 auto, 1 off, 2 on")
     a = ap.parse_args()
     if hrt._lib.lib().rt_diagnostic_build() != 1:
         raise SystemExit("not a diagnostic build: set HRT_LIB=lib/libhrt_phase.so")
     sd = CONFIGS[a.config]()
     for sb in a.suspend_below:
         r = make_renderer(sd)
-        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, fold=hrt.RT_FOLD_BUFFER, **({} if sb is None else {"suspend_below": sb}))
+        r.set_params(schedule=hrt.RT_SCHEDULE_QUEUE, fold=hrt.RT_FOLD_BUFFER, packet=a.packet,
+                     **({} if sb is None else {"suspend_below": sb}))
         r.draw_frames(2, 1000, 10)  # warm-up
         r.synchronize()
         r.draw_frames(a.frames, 1000, 10)

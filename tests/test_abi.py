@@ -104,7 +104,7 @@ def test_struct_layouts_match_header():
         got = [(f, t) for f, t in py._fields_]
         assert [f for f, _ in fields] == [f for f, _ in got], name
         assert [C.sizeof(t) for _, t in fields] == [C.sizeof(t) for _, t in got], name
-    assert C.sizeof(hrt.RtParams) == 19 * 4
+    assert C.sizeof(hrt.RtParams) == 20 * 4
     assert C.sizeof(hrt.RtStats) == 8 + 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 64 + 8 + 4 + 4 + 8 + 4 + 4
     from oracle import oracle as O
     assert [O.lib().oracle_sizeof(i) for i in range(6)] == [80, 32, 48, 32, 64, C.sizeof(O.OParams)]
@@ -136,3 +136,13 @@ def test_device_code_object_is_gfx950(tmp_path):
     text = out.stdout + out.stderr
     if "gfx950" not in text:  # older objdump: look for the bundle id string directly
         assert b"gfx950" in _lib.LIB_PATH.read_bytes()
+
+
+def test_abi_version_guard():
+    """rt_abi_version reports the header's version and the sizes rt_set_params / rt_get_stats copy."""
+    text = (Path(__file__).resolve().parents[1] / "include" / "hrt.h").read_text()
+    want = int(re.search(r"#define RT_ABI_VERSION (\d+)u", text).group(1))
+    v, pb, sb = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    assert hrt.lib().rt_abi_version(C.byref(v), C.byref(pb), C.byref(sb)) == 0
+    assert (v.value, pb.value, sb.value) == (want, C.sizeof(hrt.RtParams), C.sizeof(hrt.RtStats))
+    assert hrt.lib().rt_abi_version(None, None, None) == 0

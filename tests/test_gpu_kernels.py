@@ -61,7 +61,8 @@ def _cases():
     for sd in (c3, deep):
         for steal in (1, 2):
             for count in (0, 1):
-                cases.append((sd, dict(schedule=Q, steal=steal, count_tests=count)))
+                for packet in ((1, 2) if sd is c3 else (0,)):  # (the packet walk needs the LDS nodes: not the deep tree)
+                    cases.append((sd, dict(schedule=Q, steal=steal, count_tests=count, packet=packet)))
     for v in (1, 3):
         cases.append((c3, dict(schedule=Q, variant=v, steal=1)))
     for v in (1, 3, 4):

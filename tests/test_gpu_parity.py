@@ -132,16 +132,20 @@ def test_sample_queue_equals_tiles(case):
     sd = _schedule_cases()[case]
     for row0, step in [(0, 1), (1, 3)]:
         out = []
-        for schedule in (hrt.RT_SCHEDULE_TILES, hrt.RT_SCHEDULE_QUEUE):
+        # (packet 1: the queue's primary rays walk on their own, so the box / sphere test counts are the tiles'; the
+        # packet walk's, packet 2, count its union's tests: same bits and queries)
+        for schedule, packet in ((hrt.RT_SCHEDULE_TILES, 0), (hrt.RT_SCHEDULE_QUEUE, 1), (hrt.RT_SCHEDULE_QUEUE, 2)):
             r = scenes.make_renderer(sd)
-            r.set_params(schedule=schedule, row0=row0, row_step=step, job_frames=3)  # ragged last job
+            r.set_params(schedule=schedule, row0=row0, row_step=step, job_frames=3, packet=packet)  # ragged last job
             r.set_frame_count(3)
             r.draw_frames(sd.frames, 2000, 7)
             out.append((r.read_image(), r.stats()))
-        (a, sa), (b, sb) = out
+        (a, sa), (b, sb), (c, sc) = out
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+        np.testing.assert_array_equal(a.view(np.uint32), c.view(np.uint32))
         assert (sa.queries, sa.box_tests, sa.sphere_tests, sa.node_tests, sa.tri_tests) == \
                (sb.queries, sb.box_tests, sb.sphere_tests, sb.node_tests, sb.tri_tests)
+        assert (sc.queries, sc.node_tests, sc.tri_tests) == (sa.queries, sa.node_tests, sa.tri_tests)
         assert sb.schedule == hrt.RT_SCHEDULE_QUEUE and sb.samples == sa.samples
 
 
@@ -600,7 +604,9 @@ def test_count_tests_off_bit_identical():
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=sd.name)
         assert sa.queries == sb.queries and sa.box_tests > 0 and sa.sphere_tests > 0
         if sd.mode == hrt.RT_MODE_SPHERE:
-            assert sb.box_tests == 0 and sb.sphere_tests == 0 and sb.kernel.endswith(b"false>"), sb.kernel
+            # k_trace_split<LNODES, STEAL, COUNT, PACKET>: the uncounted instantiation
+            assert sb.box_tests == 0 and sb.sphere_tests == 0, sb.kernel
+            assert sb.kernel.decode().split("<")[1].split(", ")[2] == "false", sb.kernel
         else:
             assert (sb.box_tests, sb.sphere_tests, sb.node_tests, sb.tri_tests) == \
                 (sa.box_tests, sa.sphere_tests, sa.node_tests, sa.tri_tests)

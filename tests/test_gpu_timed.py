@@ -14,7 +14,7 @@ import pytest
 import bench
 import hrt
 import scenes
-from hrt.parallel import rank_params
+from hrt.parallel import owned_rows, rank_params
 
 pytestmark = pytest.mark.gpu
 
@@ -32,22 +32,38 @@ def assert_bits(gpu: np.ndarray, ref: np.ndarray, what: str):
     assert same.all(), f"{what}: {np.size(same) - same.sum()} channels differ (max |d| {np.nanmax(d)})"
 
 
-def timed_draw(sd, **params):
-    """One bench step (bench.py main/step): the one-rank row partition, the timed knobs, reset, draw every frame."""
+def timed_draw(sd, rank=0, world=1, block=8, warmup=1, **params):
+    """One bench step as bench.run_leg times it: this rank's row share, the timed knobs, `warmup` counting steps (they
+    learn the tiles' cost order, rt_params.cost_order), then reset and draw every frame uncounted."""
     r = scenes.make_renderer(sd)
-    r.set_params(**rank_params(0, 1, 8), **bench.timed_knobs(**params))
+    r.set_params(**rank_params(rank, world, block), **bench.timed_knobs(**params))
+    for _ in range(warmup):  # (bench.run_leg counting_step)
+        r.set_params(count_tests=1)
+        r.reset_frame_count()
+        r.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
+        r.set_params(count_tests=0)
     r.reset_frame_count()
     r.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
     return r, r.read_image(), r.stats()
+
+
+def composition(st) -> tuple:
+    """What the bench line reports of a timed step's launches."""
+    return st.kernel.decode(), st.trace_launches, st.launch_frames, st.ordered_launches, st.fold_ring
+
+
+def local_row(rank, world, block, height, row) -> int:
+    rows = list(owned_rows(block * rank, world, height, block))
+    return rows.index(row)
 
 
 def test_c3_as_timed_crosses_the_ema_switch_inside_a_launch():
     sd = scenes.config_c3()
     assert (sd.width, sd.height, sd.frames) == (1920, 1080, 1024)
     r, img, st = timed_draw(sd)
-    # the composition of the bench line (BENCH_r04: kernel, launch_frames 352, 3 launches per step)
-    assert st.kernel.decode() == "k_trace_split<true, false, false>", st.kernel
-    assert (st.trace_launches, st.launch_frames, st.fold_ring) == (3, 352, 0), (st.trace_launches, st.launch_frames)
+    # the composition of the bench line (kernel, 3 launches of 352 frames per step, all three dealt in the cost order
+    # the warmup step learnt)
+    assert composition(st) == ("k_trace_split<true, false, false, false>", 3, 352, 3, 0), composition(st)
     assert st.box_tests == 0 and st.sphere_tests == 0  # uncounted, as timed
     assert 704 < 1000 < 1024  # frame 1000 is folded by the third launch's k_accumulate
     rows = (7, 536, 3)  # rows 7, 543, 1079
@@ -59,7 +75,7 @@ def test_c3_as_timed_crosses_the_ema_switch_inside_a_launch():
     r2.set_params(row0=7, row_step=536, row_block=1, **bench.timed_knobs(queue_budget_mb=62, steal=1))
     r2.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
     st2 = r2.stats()
-    assert st2.kernel.decode() == "k_trace_split<true, false, false>" and st2.trace_launches == 3
+    assert st2.kernel.decode() == "k_trace_split<true, false, false, false>" and st2.trace_launches == 3
     assert st2.launch_frames == 352
     _, q = scenes.oracle_render(sd, rows=rows)
     assert st2.queries == q
@@ -69,9 +85,8 @@ def test_c3_as_timed_crosses_the_ema_switch_inside_a_launch():
 def test_c4_as_timed():
     sd = scenes.config_c4()
     assert (sd.width, sd.height, sd.frames) == (1920, 1080, 512)
-    r, img, st = timed_draw(sd)
-    assert st.kernel.decode() == "k_trace_split_tris<2, 1, 3, false>", st.kernel
-    assert (st.trace_launches, st.launch_frames, st.fold_ring) == (1, 512, 0)
+    r, img, st = timed_draw(sd, block=4)
+    assert composition(st) == ("k_trace_split_tris<2, 1, 3, false>", 1, 512, 1, 0), composition(st)
     ref, _ = scenes.oracle_render(sd, rows=(452, 160, 2))  # rows 452, 612: Suzanne and the ground
     assert_bits(img[452:613:160], ref, "C4 timed composition, rows 452 / 612 x 512 frames")
 
@@ -92,3 +107,36 @@ def test_c5_as_timed_in_twelve_launches():
     x0, nx = 1664, 512
     ref, _ = scenes.oracle_render(sd, rows=(1080, 1, 1), x0=x0, nx=nx)
     assert_bits(img[:, x0:x0 + nx], ref, "C5 timed composition, row 1080, columns 1664-2175 x 4096 frames")
+
+
+def test_c3_rank_share_as_timed_at_eight_ranks():
+    """The share the driver's 8-GPU run times on rank 4: rows dealt in 8-row blocks, one 1024-frame
+    launch, dealt in the cost order the counting warmup step learnt (no stealing once learnt). Global row 547
+    (local row 67) against the oracle at all 1024 frames."""
+    sd = scenes.config_c3()
+    r, img, st = timed_draw(sd, rank=4, world=8, block=8)
+    assert composition(st) == ("k_trace_split<true, false, false, false>", 1, 1024, 1, 0), composition(st)
+    k = local_row(4, 8, 8, sd.height, 547)
+    ref, _ = scenes.oracle_render(sd, rows=(547, 1, 1))
+    assert_bits(img[k:k + 1], ref, "C3 rank 4 of 8, row 547 x 1024 frames")
+
+
+def test_c4_rank_share_as_timed_at_eight_ranks():
+    """C4's 8-rank share (4-row blocks, bench.ROW_BLOCK): rank 3, global row 524 (Suzanne) at all 512 frames."""
+    sd = scenes.config_c4()
+    r, img, st = timed_draw(sd, rank=3, world=8, block=4)
+    assert composition(st) == ("k_trace_split_tris<2, 1, 3, false>", 1, 512, 1, 0), composition(st)
+    k = local_row(3, 8, 4, sd.height, 524)
+    ref, _ = scenes.oracle_render(sd, rows=(524, 1, 1))
+    assert_bits(img[k:k + 1], ref, "C4 rank 3 of 8, row 524 x 512 frames")
+
+
+def test_c2_as_timed():
+    """C2 (the linear sphere scan, k_trace) at 256 spp: one launch, raster order (cost order is for the suspendable-walk
+    kernels' full images and the ranks' shares). Rows 200 (the three spheres) and 500 (the ground) at all frames."""
+    sd = scenes.config_c2()
+    assert (sd.width, sd.height, sd.frames) == (1280, 720, 256)
+    r, img, st = timed_draw(sd)
+    assert composition(st) == ("k_trace<0, 1, false>", 1, 256, 0, 0), composition(st)
+    ref, _ = scenes.oracle_render(sd, rows=(200, 300, 2))
+    assert_bits(img[200:501:300], ref, "C2 timed composition, rows 200 / 500 x 256 frames")
