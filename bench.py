@@ -279,6 +279,11 @@ def cpu_baseline(sd, threads: int, rows: int, frames: int):
         "algorithm": (f"linear-scan oracle: every ray tests all {len(sd.spheres)} sphere slots (the reference's "
                       "algorithm); the GPU kernel culls with a BVH, so the ratio mixes algorithm and hardware"),
         "threads": threads,
+        # (why not every core) the GPU box gives one GPU's job a 16-thread CPU share (OMP_NUM_THREADS=16 on
+        # the pool; the machine's other cores belong to the other GPUs' jobs), so the baseline uses that share; per core:
+        "value_per_core": round(q / dt / 1e6 / threads, 3),
+        "cores_note": "16 = the CPU share of one GPU on the box (the visible cores serve 8 GPUs' jobs); scale "
+                      "value_per_core by a core count for other hosts",
         **cpu_info(),
         "sample": f"{sd.name}: {n} rows (every {step}th) x {sd.width} px x {frames} frames, {q} rays in {dt:.1f} s",
     }
@@ -516,6 +521,7 @@ def main() -> int:
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU-only rehearsal of the multi-rank path (self-launch, gloo, row-tile gather): no GPU")
     args = ap.parse_args()
+    args.row_block_given = args.row_block is not None  # (the C5 leg keeps its own partition unless one was given)
     if args.row_block is None:
         args.row_block = ROW_BLOCK.get(args.config, 8)
 
@@ -611,12 +617,18 @@ def main() -> int:
     c5 = None
     c5_on = args.c5_leg if args.c5_leg is not None else (world > 1 and args.config != "c5")
     if c5_on:
+        # the headline leg's renderer (and its colour buffer) goes first: one leg's memory at a time
+        del L["renderer"]
+        torch.cuda.synchronize()
         sd5 = scenes.CONFIGS["c5"]()
+        head_block = args.row_block
+        args.row_block = args.row_block if args.row_block_given else ROW_BLOCK.get("c5", 8)
         L5 = run_leg(sd5, timed_knobs(args.frames_per_launch, 0, 0, 0), args, dist, rank, world, dev, args.c5_steps,
                      args.c5_warmup, tag="c5")
         rep5 = rank_reports(L5["local"], world, dist, coll_dev)
-        c5 = {"L": L5, "report": rep5, "sd": sd5}
+        c5 = {"L": L5, "report": rep5, "sd": sd5, "row_block": args.row_block}
         del L5["renderer"]
+        args.row_block = head_block
 
     device_error = None
     if rank == 0:
@@ -685,6 +697,9 @@ def main() -> int:
                 "launch_frames": int(st_last.launch_frames) if schedule == 2 else 0,
                 # trace launches of the last timed step that dealt their tiles in learnt cost order (rt_params.cost_order)
                 "ordered_launches": int(st_last.ordered_launches) if schedule == 2 else 0,
+                # the timed steps redraw the warmup's scene: tile costs learnt before the timed region (a cold single
+                # render runs 1 learning + 2 ordered launches for C3, ~0.6 % slower)
+                "warm": bool(args.warmup > 0 and schedule == 2 and st_last.ordered_launches > 0),
             },
             # The path is FP32-VALU issue bound (no MFMA: no dense contraction; HBM ~2 % busy). `achieved` =
             # the FP32 FLOPs the kernel executes (its exact in-kernel test counters x FLOP per test, + the
@@ -743,7 +758,7 @@ def main() -> int:
                 "ms_per_step": round(t5 / max(args.c5_steps, 1) * 1e3, 2),
                 "config": {"workload": sd5.name, "id": "c5", "width": sd5.width, "height": sd5.height, "spp": sd5.frames,
                            "bounces": sd5.bounces, "spheres": len(sd5.spheres), "parallelism": f"rows{world}",
-                           "row_block": args.row_block, "rays_per_step": round(q5 / max(args.c5_steps, 1)),
+                           "row_block": c5["row_block"], "rays_per_step": round(q5 / max(args.c5_steps, 1)),
                            "kernel": st5.kernel.decode() if st5 is not None else "",
                            "launch_frames": int(st5.launch_frames) if st5 is not None else 0,
                            "trace_launches_per_step": int(st5.trace_launches) if st5 is not None else 0},

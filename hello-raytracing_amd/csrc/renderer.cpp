@@ -538,7 +538,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 #ifdef HRT_STAMPS
     {
         // k_render's waves, or the persistent kernels' (at most steal_cap = 32 per CU)
-        const size_t words = 4ull * std::max<size_t>((size_t)((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u,
+        const size_t words = 8ull * std::max<size_t>((size_t)((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u,
                                                      32ull * std::max(r->cus, 1u));
         int rc2 = ensure(r->wave_trace, words);
         if (rc2) return rc2;
@@ -733,7 +733,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 #ifndef HRT_NQ
 #define HRT_NQ 1
 #endif
-        constexpr size_t QWORDS = 8u * 16u;  // NQ x QSTRIDE
+        constexpr size_t QWORDS = (size_t)hrt_dev::NQ * hrt_dev::QSTRIDE;
         P.queues = nullptr;
         if (HRT_NQ && !P.ring_mode) {
             rc = ensure(r->queues, QWORDS);
@@ -999,7 +999,7 @@ int rt_create(uint32_t width, uint32_t height, int mode, rt_renderer** out) {
     r->params.row_block = 1;
     r->params.frames_per_launch = 32;
     r->params.schedule = RT_SCHEDULE_AUTO;
-    // auto: balanced launches of 320-639 frames (C3: 3 x 342 frames, 8.5 GB of colours; launch_frames)
+    // auto: balanced launches of 320-639 frames of whole jobs (C3: 352 + 352 + 320 frames, 8.8 GB of colours; launch_frames)
     r->params.queue_budget_mb = 0;
     // frames per 8x8-tile job; measured with the frame-block refill: C2 59.5 (8) -> 69.1 (16) -> 68.2 (32),
     // C3 +1 % at 16, C4 equal at 8/16 and -13 % at 32, C5 +0.7 % at 16

@@ -86,6 +86,9 @@ constexpr uint32_t WATCHDOG = 16, COUNTER_WORDS = 20;
 #define HRT_CSPREAD 64
 #endif
 constexpr uint32_t CSPREAD = HRT_CSPREAD, CSTRIDE = 16;
+// the sample buffer's job queue: NQ counters (one per XCD of MI355X's 8), QSTRIDE words apart (rt_kernels.hip queue_take;
+// renderer.cpp allocates and zeroes NQ x QSTRIDE words)
+constexpr uint32_t NQ = 8, QSTRIDE = 16;
 
 // fold ring: jobs per tile and launch (the done bits of a tile's fold word, rt_kernels.hip)
 constexpr uint32_t FOLD_MAX_JOBS = 48;

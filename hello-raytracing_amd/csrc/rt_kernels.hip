@@ -1726,7 +1726,7 @@ __device__ __forceinline__ bool slot_poll(const WaveJobs& J, uint32_t flags, uin
 // its XCD's queue first, then from the others in turn (the queues it found exhausted kept in its WJ_QDEAD word: the
 // ring's slot words, unused with the sample buffer). With one counter for the whole GPU every job fetch is an atomic
 // on one address from every XCD. Lane 0; returns >= njobs when every queue is exhausted.
-constexpr uint32_t NQ = 8, QSTRIDE = 16, WJ_QDEAD = WJ_SLOT;
+constexpr uint32_t WJ_QDEAD = WJ_SLOT;  // (NQ, QSTRIDE: rt_device.hpp)
 __device__ __forceinline__ uint32_t queue_take_lane0(const WaveJobs& J, const KPtr K) {
     unsigned long long* const qs = K->queues;
     if (qs == nullptr) return (uint32_t)min(atomicAdd(K->queue, 1ull), 0xFFFFFFFFull);
@@ -1907,12 +1907,7 @@ enum : uint32_t { WJ_ST = WJ_TILE, WJ_VICTIM = WJ_TILE + 1, WJ_PRIV_F = WJ_TILE 
 __device__ __forceinline__ bool queue_drained(const WaveJobs& J, uint32_t lane) {
     if (J.get(WJ_ST) & ST_QEMPTY) return true;
     const KPtr K = kargs();
-    if (unsigned long long* const qs = K->queues) {  // every queue exhausted (lane q reads queue q)
-        bool done = true;
-        if (lane < NQ)
-            done = __hip_atomic_load(qs + lane * QSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * NQ + lane >= K->njobs;
-        return __ballot(!done) == 0ull;
-    }
+    // (stealing launches run on the single counter: renderer.cpp gives them no per-XCD queues)
     uint32_t d = 0;
     if (lane == 0) d = __hip_atomic_load(K->queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= K->njobs ? 1u : 0u;
     return uniform(__shfl(d, 0)) != 0u;
@@ -2035,6 +2030,7 @@ struct BlockQueue {
     uint32_t njobs = 0;                // (diagnostic build: jobs this wave took, when it took its last one, and
     unsigned long long last_job = 0;   // the longest time between two of its job fetches)
     unsigned long long max_job = 0;
+    uint32_t took_job = 0;             // (a job was taken this round)
 #endif
 };
 
@@ -2059,6 +2055,7 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
                     if (B.njobs) B.max_job = max(B.max_job, now - B.last_job);
                     B.njobs++;
                     B.last_job = now;
+                    B.took_job = 1u;
                 }
 #endif
             }
@@ -2225,7 +2222,7 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
                 asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
                 asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
                 const size_t wid = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4u + wave;
-                unsigned long long* rec = P.wave_trace + 4u * wid;
+                unsigned long long* rec = P.wave_trace + 8u * wid;  // (8-word records, WaveRecord; words 4-7 unused here)
                 rec[0] = rt_start;
                 rec[1] = r1;
                 rec[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
@@ -2261,14 +2258,39 @@ __global__ __launch_bounds__(256) void k_render(const KParams P) {
 // mix (shader_sphere.wgsl:264-271; fold_session), so the image is bit-identical to k_render's and to
 // count x rt_draw.
 #ifdef HRT_STAMPS
-// Diagnostic build: the persistent kernels' per-wave record (rt_get_wave_trace; scripts/wave_tail.py), 4 words per wave
+// Diagnostic build: the persistent kernels' per-wave record (rt_get_wave_trace; scripts/wave_tail.py), 8 words per wave
 // at wave id blockIdx.x * waves per workgroup + wave: start and end (100 MHz ticks, s_memrealtime), HW_ID | XCC_ID << 32,
 // and (ticks from start until the wave first found no frame block left to take) | frame blocks it generated << 32.
 struct WaveRecord {
-    unsigned long long start = 0, drained = 0;
-    __device__ void begin() { start = hrt_realtime(); }
-    __device__ void drain(bool d) {
-        if (d && drained == 0ull) drained = hrt_realtime() - start;
+    // 8 words per wave (rt_get_wave_trace): [0] start, [1] end (s_memrealtime, 100 MHz); [2] HW_ID (k_trace: the longest
+    // job in bits 0-23) | XCC_ID << 32 | k_trace: the last job's take << 40; [3] ticks until the wave first found no work |
+    // frame blocks generated << 32 (k_trace: jobs taken); [4] / [5] s_memtime (shader clock) at start / end; [6] shader
+    // clock ticks from start to the drain (0: never drained) | k_trace: to its last job take << 32; [7] k_trace: lanes
+    // holding a sample at the drain | samples finished after the last job take << 8 | rounds after the drain << 24 |
+    // rounds from the last job take to the drain << 36 | all rounds << 48 (the C2 launch-end tail)
+    unsigned long long start = 0, drained = 0, start_clk = 0, drained_clk = 0, job_clk = 0;
+    uint32_t inflight = 0, fin_after_job = 0, rounds_after_drain = 0, rounds_job = 0, rounds = 0;
+    __device__ void begin() {
+        start = hrt_realtime();
+        start_clk = hrt_stamp();
+    }
+    __device__ void drain(bool d, uint32_t in_flight = 0) {
+        if (d && drained == 0ull) {
+            drained = hrt_realtime() - start;
+            drained_clk = hrt_stamp();
+            inflight = in_flight;
+        }
+    }
+    __device__ void round(uint32_t finished, bool took_job) {  // (k_trace: once per round, wave-uniform)
+        rounds++;
+        if (took_job) {
+            fin_after_job = 0;
+            rounds_job = 0;
+            job_clk = hrt_stamp();
+        }
+        fin_after_job += finished;
+        if (drained) rounds_after_drain++;
+        else rounds_job++;
     }
     // last_job (k_trace): when the wave took its last job (s_memrealtime; 0: not recorded), as ticks from its start in
     // bits 40-63 of word 2
@@ -2276,18 +2298,25 @@ struct WaveRecord {
     __device__ void finish(const KParams& P, uint32_t lane, uint32_t nblocks, unsigned long long last_job = 0,
                            unsigned long long max_job = 0) {
         if (lane != 0u || P.wave_trace == nullptr) return;
-        const unsigned long long end = hrt_realtime();
+        const unsigned long long end = hrt_realtime(), end_clk = hrt_stamp();
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         const size_t wid = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        unsigned long long* rec = P.wave_trace + 4u * wid;
+        unsigned long long* rec = P.wave_trace + 8u * wid;
         rec[0] = start;
         rec[1] = end;
         const unsigned long long lj = last_job ? min(last_job - start, 0xFFFFFFull) : 0ull;
         const unsigned long long w0 = last_job ? min(max_job, 0xFFFFFFull) : (unsigned long long)hw;
         rec[2] = w0 | ((unsigned long long)(xcc & 0xFFu) << 32) | (lj << 40);
         rec[3] = (drained ? drained : end - start) | ((unsigned long long)nblocks << 32);
+        rec[4] = start_clk;
+        rec[5] = end_clk;
+        rec[6] = (drained_clk ? min(drained_clk - start_clk, 0xFFFFFFFFull) : 0ull) |
+                 ((job_clk ? min(job_clk - start_clk, 0xFFFFFFFFull) : 0ull) << 32);
+        rec[7] = (unsigned long long)min(inflight, 0xFFu) | ((unsigned long long)min(fin_after_job, 0xFFFFu) << 8) |
+                 ((unsigned long long)min(rounds_after_drain, 0xFFFu) << 24) | ((unsigned long long)min(rounds_job, 0xFFFu) << 36) |
+                 ((unsigned long long)min(rounds, 0xFFFFu) << 48);
     }
 };
 #endif
@@ -2387,7 +2416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #ifdef HRT_STAMPS
         st_tb = hrt_stamp();
         if (have) st_gen += st_tb - st_ta;
-        wrec.drain(drained);
+        wrec.drain(drained, (uint32_t)__popcll(__ballot(have)));
 #endif
         if (__ballot(have) == 0ull) {
             if (drained && J.idle()) break;
@@ -2430,6 +2459,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         }
 #ifdef HRT_STAMPS
         st_shade += hrt_stamp() - st_tb;
+        wrec.round((uint32_t)__popcll(__ballot(fin)), BQ.took_job != 0u);
+        BQ.took_job = 0u;
 #endif
         job_account(J, fin, fl, lane);
     }
@@ -2671,6 +2702,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
     uint32_t* const stack = bvh_stack + threadIdx.x;
     Tally tally;
     uint32_t queries = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t suspend_below = P.suspend_below;
 
     bool drained = false;
@@ -2787,7 +2819,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const uint32_t avail = 64u - blk_next;
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // (PACKET: the rank by mbcnt, no 64-bit lane mask held in VGPRs — the packet kernel's register budget; the
+            // other instantiations keep the mask: same-box A/B, the mbcnt form cost C3 0.3 %)
+            const uint32_t rank = PACKET ? __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))
+                                         : (uint32_t)__popcll(m & below);
             const int src = (int)((blk_next + rank) & 63u);
             const float4 b0 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src)];
             const float4 b1 = blk[2 * ((threadIdx.x & ~63u) + (uint32_t)src) + 1];
@@ -2854,8 +2889,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
         }
         HRT_PHASE(2);
         HRT_LANES(2, have && qs >= 2u);
-        // (the queries shaded this round, counted per wave: a wave-uniform count needs no VGPR)
-        queries += (uint32_t)__popcll(__ballot(have && (qs == 2u || (PACKET && qs == 4u))));
+        // (PACKET: the queries shaded this round counted per wave — a wave-uniform count needs no VGPR; the others count
+        // per lane, as before)
+        if constexpr (PACKET) queries += (uint32_t)__popcll(__ballot(have && (qs == 2u || qs == 4u)));
         if (have && qs >= 2u) {
 #ifdef HRT_STAMPS
             tally.lshade++;
@@ -2873,6 +2909,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
                     bi = bvh_end<true>(P, ray, Q, best, tally);
                     p = point_on_ray(ray.o, ray.d, best);
                 }
+                if constexpr (!PACKET) queries++;
                 if (bi >= 0) {
                     Hit h;
                     sphere_record_p(P, p, ray.d, bi, best, h);
@@ -2916,7 +2953,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
     if (lane == 0)
         for (uint32_t c = 0; c < 4u; c++) atomicAdd(P.counter + 5 + c, (unsigned long long)J.get(WJ_STAT + c));
 #endif
-    unsigned long long sums[5] = {lane == 0u ? queries : 0u, tally.boxes, tally.spheres, tally.nodes, tally.tris};
+    unsigned long long sums[5] = {(!PACKET || lane == 0u) ? queries : 0u, tally.boxes, tally.spheres, tally.nodes, tally.tris};
 #pragma unroll
     for (int c = 0; c < 5; c++) {
 #pragma unroll

@@ -238,11 +238,12 @@ int rt_release_scratch(rt_renderer *r);
 #define RT_RAW_COUNTERS 16
 int rt_get_raw_counters(const rt_renderer *r, uint64_t *out, int n);
 int rt_diagnostic_build(void);
-/* Diagnostic build: per-wave records of the last launch of the last draw, 4 words per wave: start and end
- * (100 MHz ticks), HW_ID | XCC_ID << 32, then for the tiles kernel (k_render; waves in
- * (blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave order) the closest-hit queries of lane 0's pixel, for the
- * suspendable-walk kernels (waves in blockIdx.x * waves per workgroup + wave order) the ticks until the wave first
- * found no frame block left | the frame blocks it generated << 32. Zero words in the product build. */
+/* Diagnostic build: per-wave records of the last launch of the last draw, 8 words per wave (waves in blockIdx.x *
+ * waves per workgroup + wave order): start and end (s_memrealtime, 100 MHz ticks); HW_ID | XCC_ID << 32 (k_trace: the
+ * longest time between two job takes in bits 0-23, its last job take << 40); the ticks until the wave first found no
+ * work left | the frame blocks it generated << 32 (k_trace: the JOBS it took); the shader clock (s_memtime) at start,
+ * end and that first drain; k_trace: lanes holding a sample at the drain | samples finished after the last job take
+ * << 16 | rounds after the drain << 40 (scripts/wave_tail.py). Zero words in the product build. */
 int rt_get_wave_trace(rt_renderer *r, uint64_t *out, size_t n_words);
 
 /* Self-check of the kernels' range-restricted correctly rounded sqrt / division sequences against the IEEE

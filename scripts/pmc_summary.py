@@ -14,9 +14,11 @@ import sys
 
 out = sys.argv[1]
 key = None
+line_json = None
 try:
     line = [ln for ln in open(f"{out}/p1.log") if ln.startswith("{")][-1]
     b = json.loads(line)
+    line_json = b
     key = {"config": b["config"]["id"], "width": b["config"]["width"], "height": b["config"]["height"],
            "spp": b["config"]["spp"], "ranks": b["n_gpus"], "kernel": b["roofline"]["kernel"]}
 except (OSError, IndexError, KeyError, ValueError):
@@ -40,6 +42,19 @@ for f in sorted(glob.glob(f"{out}/**/p*_counter_collection.csv", recursive=True)
         dk = (f, r["Dispatch_Id"])
         per[dk][r["Counter_Name"]] += float(r["Counter_Value"])
         names[dk] = r["Kernel_Name"]
+# The timed launches only (round 6): a bench run's warmup step learns the tiles' cost order, and its learning launch also
+# writes every sample's query count to a per-pixel counter — C4: 19.5 GB of writes against the timed launch's 13.5 GB
+# (profiles/r06/c4_learning_vs_timed.txt). Averaging it in made round 5's C4 summary read 15.0 GB. PMC_DISPATCH=timed
+# (the default) keeps each pass's last `launches_per_step` x `steps` dispatches of the kernel (the bench line's timed
+# steps; run the passes with --emulate-ranks 0); PMC_DISPATCH=all averages every dispatch.
+import os  # noqa: E402
+if os.environ.get("PMC_DISPATCH", "timed") == "timed" and line_json is not None:
+    keep = int(round(line_json["roofline"].get("launches_per_step", 1) * line_json.get("steps", 1)))
+    by_file = collections.defaultdict(list)
+    for f, d in per:
+        by_file[f].append(int(d))
+    last = {f: set(sorted(ds)[-keep:]) for f, ds in by_file.items()}
+    per = {dk: cs for dk, cs in per.items() if int(dk[1]) in last[dk[0]]}
 agg = collections.defaultdict(list)
 for dk, cs in per.items():
     for c, v in cs.items():

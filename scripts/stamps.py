@@ -91,10 +91,10 @@ def main() -> None:
         }
         if a.trace and a.schedule == 1:
             import numpy as np
-            nw = 4 * ((sd.width + 15) // 16) * ((sd.height + 15) // 16) * 4
+            nw = 8 * ((sd.width + 15) // 16) * ((sd.height + 15) // 16) * 4
             buf = (hrt._lib.C.c_uint64 * nw)()
             hrt._lib.check(L.rt_get_wave_trace(r._h, buf, nw), "wave_trace")
-            tr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).copy()
+            tr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[:, :4].copy()
             name = os.path.join(a.trace, f"trace_{a.config}_v{v}_f{fpl}.npy")
             np.save(name, tr)
             row.update(trace_summary(tr))

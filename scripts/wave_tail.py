@@ -33,7 +33,9 @@ def summarise(tr: np.ndarray) -> dict:
     ok = en > 0
     st, en, info = st[ok], en[ok], tr[ok, 3].astype(np.int64)
     drained = info & 0xFFFFFFFF
-    blocks = info >> 32
+    blocks = info >> 32  # frame blocks generated (split kernels) or jobs taken (k_trace)
+    clk0, clk1, w6, w7 = (tr[ok, k].astype(np.int64) for k in (4, 5, 6, 7))
+    dclk, jclk = w6 & 0xFFFFFFFF, w6 >> 32  # shader-clock ticks from start to the drain / to the last job take
     last_job = (tr[ok, 2].astype(np.uint64) >> np.uint64(40)).astype(np.int64)  # k_trace: when the last job was taken
     t0 = st.min()
     span = (en.max() - t0) / 1e5
@@ -50,12 +52,25 @@ def summarise(tr: np.ndarray) -> dict:
         "drain_ms_pcts": pct((st + drained - t0) / 1e5),
         "end_ms_pcts": pct((en - t0) / 1e5),
         "tail_after_first_drain_ms": round(float((en.max() - (st + drained).min()) / 1e5), 3),
-        "blocks_per_wave_pcts": pct(blocks),  # (k_trace: jobs per wave)
+        ("jobs_per_wave_pcts" if last_job.any() else "blocks_per_wave_pcts"): pct(blocks),
         "last_job_ms_pcts": pct((st + last_job - t0) / 1e5) if last_job.any() else None,
         "last_job_to_end_ms_pcts": pct((en - st - last_job) / 1e5) if last_job.any() else None,
         # k_trace: the longest time between two of the wave's job fetches (its longest job but the last)
         "max_job_ms_pcts": pct((tr[ok, 2].astype(np.int64) & 0xFFFFFF) / 1e5) if last_job.any() else None,
-        "blocks_total": int(blocks.sum()),
+        ("jobs_total" if last_job.any() else "blocks_total"): int(blocks.sum()),
+        # shader clock (s_memtime ticks per s_memrealtime tick x 100 MHz) over each wave's life and after its drain
+        "clock_mhz_pcts": pct((clk1 - clk0) / np.maximum(en - st, 1) * 100.0),
+        "clock_mhz_after_drain_pcts": pct((clk1 - clk0 - dclk)[dclk > 0] / np.maximum((en - st - drained)[dclk > 0], 1) * 100.0)
+        if (dclk > 0).any() else None,
+        # k_trace: lanes holding a sample when the wave found the queue drained, samples finished after its last job take,
+        # rounds after the drain, rounds from the last job take to the drain, shader cycles per round then and overall
+        "inflight_at_drain_pcts": pct(w7 & 0xFF) if last_job.any() else None,
+        "finished_after_last_job_pcts": pct((w7 >> 8) & 0xFFFF) if last_job.any() else None,
+        "rounds_after_drain_pcts": pct((w7 >> 24) & 0xFFF) if last_job.any() else None,
+        "rounds_in_last_job_pcts": pct((w7 >> 36) & 0xFFF) if last_job.any() else None,
+        "clk_per_round_last_job_pcts": pct((dclk - jclk)[dclk > 0] / np.maximum((w7 >> 36) & 0xFFF, 1)[dclk > 0])
+        if last_job.any() and (dclk > 0).any() else None,
+        "clk_per_round_overall_pcts": pct((clk1 - clk0) / np.maximum(w7 >> 48, 1)) if last_job.any() else None,
         "resident_waves_timeline": conc,
     }
 
@@ -73,10 +88,10 @@ def draw(sd, params: dict):
     st = r.stats()
     wall = time.perf_counter() - t
     import ctypes as C
-    words = 4 * 32 * 256
+    words = 8 * 32 * 256
     buf = (C.c_uint64 * words)()
     hrt._lib.check(hrt.lib().rt_get_wave_trace(r._h, buf, words), "rt_get_wave_trace")
-    tr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    tr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
     out = {"kernel": st.kernel.decode(), "trace_ms": round(st.trace_ms, 3), "kernel_ms": round(st.kernel_ms, 3),
            "wall_ms": round(wall * 1e3, 3), "trace_launches": st.trace_launches, "rays": st.queries}
     out.update(summarise(tr))
