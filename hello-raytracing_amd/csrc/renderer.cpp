@@ -538,13 +538,15 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 #ifdef HRT_STAMPS
     {
         // k_render's waves, or the persistent kernels' (at most steal_cap = 32 per CU)
-        const size_t words = 8ull * std::max<size_t>((size_t)((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u,
-                                                     32ull * std::max(r->cus, 1u));
+        const size_t wave_words = 8ull * std::max<size_t>((size_t)((r->width + 15u) / 16u) * ((P.nrows + 15u) / 16u) * 4u,
+                                                          32ull * std::max(r->cus, 1u));
+        const size_t words = wave_words + (1ull << 21);  // + one word per job (k_trace's job_trace)
         int rc2 = ensure(r->wave_trace, words);
         if (rc2) return rc2;
         HIP_TRY(hipMemsetAsync(r->wave_trace.ptr, 0, words * sizeof(unsigned long long), r->stream));
         r->wave_trace_words = words;
         P.wave_trace = r->wave_trace.ptr;
+        P.job_trace = r->wave_trace.ptr + wave_words;
     }
 #endif
     const hrt::SphereBvh& B = r->bvh_host;

@@ -151,7 +151,10 @@ struct KParams {
     const TriDev* tris;
     const MatDev* mats;
     unsigned long long* counter;  // [0] closest-hit queries, [1] box tests, [2] exact sphere tests
-    unsigned long long* wave_trace;  // diagnostic build: 4 words per wave (start, end, hw ids, queries)
+    unsigned long long* wave_trace;  // diagnostic build: 8 words per wave (rt_kernels.hip WaveRecord)
+    // diagnostic build: per job (tile * nchunks + chunk, < 2^21), k_trace: the ticks from its take to the wave's next take
+    // (or drain) | the take's s_memrealtime low 32 bits << 32
+    unsigned long long* job_trace;
     // sample-queue schedule (k_trace, k_trace_split, k_trace_split_tris). Two ways to fold the sample colours
     // into the image in frame order: the sample buffer (ring_mode 0: every colour of the launch, folded by
     // k_accumulate after it; fastest, memory O(frames x pixels)) or the fold ring (ring_mode 1: a job's samples go

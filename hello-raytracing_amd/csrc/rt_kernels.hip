@@ -169,6 +169,9 @@ __device__ __forceinline__ int scan_spheres_deferred(const KParams& P, const Ray
 // the counters (wave id % CSPREAD). One set of counters for every wave made the launch's last ~1 ms a queue of
 // same-address atomics (C2: 6144 waves x 5).
 __device__ __forceinline__ void flush_counts(const unsigned long long (&sums)[5]) {
+#if defined(HRT_STAMPS) && defined(HRT_DIAG_NOFLUSH)  // (timing-only diagnostic build: no work counters)
+    if (sums[0] != ~0ull) return;
+#endif
     // (any spread of the waves over the copies will do: the wave's hardware slot — wave, SIMD, CU, shader engine in
     // HW_ID, a scalar read here — and its workgroup; threadIdx-based indices kept a VGPR alive across the kernel)
     unsigned hw;
@@ -1580,6 +1583,9 @@ __device__ __forceinline__ void ring_store(const WaveJobs& J, uint32_t pix, uint
     if (!K->ring_mode) {  // sample buffer: the colour at its frame of the launch, folded by k_accumulate
         const uint32_t npix = K->tiles_w * K->tiles_h * 64u;  // tile-padded pixels of a frame (< 2^32)
         float* o = K->samples + ((unsigned long long)ref * npix + pix) * 3u;  // one 32 x 32 + 64 multiply-add
+#if defined(HRT_STAMPS) && defined(HRT_DIAG_NOSTORE)  // (timing-only diagnostic build: wrong images)
+        if (c.x != -12345.0f) return;
+#endif
         o[0] = c.x;
         o[1] = c.y;
         o[2] = c.z;
@@ -2022,6 +2028,14 @@ __device__ __forceinline__ bool steal_drained(const WaveJobs& J) { return (J.get
 // the next frame at once (all lanes busy), and lanes that need a sample fetch one from the block's owner
 // lane with cross-lane reads, instead of each freed lane computing its own with a few lanes active
 // (k_trace_split does the same inline).
+#ifdef HRT_STAMPS
+constexpr uint32_t JOB_TRACE_CAP = 1u << 21;
+// the job's duration (take to the next take or the drain, 100 MHz ticks) | its take time's low 32 bits << 32
+__device__ __forceinline__ void job_trace_put(const KParams& P, uint32_t id, unsigned long long t0, unsigned long long t1) {
+    if (P.job_trace == nullptr || id >= JOB_TRACE_CAP || (threadIdx.x & 63u) != 0u) return;
+    P.job_trace[id] = min(t1 - t0, 0xFFFFFFFFull) | (t0 << 32);
+}
+#endif
 struct BlockQueue {
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
     f3 pr_o = {0.0f, 0.0f, 0.0f}, pr_d = {0.0f, 0.0f, 0.0f};
@@ -2031,6 +2045,7 @@ struct BlockQueue {
     unsigned long long last_job = 0;   // the longest time between two of its job fetches)
     unsigned long long max_job = 0;
     uint32_t took_job = 0;             // (a job was taken this round)
+    uint32_t job_id = 0xFFFFFFFFu;     // (the current job's index, for P.job_trace)
 #endif
 };
 
@@ -2049,13 +2064,19 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             } else {
                 if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
+#ifdef HRT_TAIL_PRIO  // (experiment: a wave holding one of the launch's last jobs issues ahead of the others)
+                if (B.job_tile + P.nwaves / max(P.nchunks, 1u) >= P.tiles_w * P.tiles_h)  // (raster order: full images)
+                    __builtin_amdgcn_s_setprio(3);
+#endif
 #ifdef HRT_STAMPS
                 {
                     const unsigned long long now = hrt_realtime();
                     if (B.njobs) B.max_job = max(B.max_job, now - B.last_job);
+                    job_trace_put(P, B.job_id, B.last_job, now);
                     B.njobs++;
                     B.last_job = now;
                     B.took_job = 1u;
+                    B.job_id = B.job_tile * P.nchunks + B.job_f0 / max(P.job_frames, 1u);
                 }
 #endif
             }
@@ -2416,6 +2437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #ifdef HRT_STAMPS
         st_tb = hrt_stamp();
         if (have) st_gen += st_tb - st_ta;
+        if (drained && wrec.drained == 0ull && BQ.job_id != 0xFFFFFFFFu) job_trace_put(P, BQ.job_id, BQ.last_job, hrt_realtime());
         wrec.drain(drained, (uint32_t)__popcll(__ballot(have)));
 #endif
         if (__ballot(have) == 0ull) {

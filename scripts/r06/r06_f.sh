@@ -10,5 +10,5 @@ python3 - "gpurun_out/$tag/wave_tail_c2.log" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 for k, v in d.items():
-    print(k, {kk: vv for kk, vv in v.items() if kk not in ("resident_waves_timeline",)})
+    print(k, json.dumps({kk: vv for kk, vv in v.items() if kk not in ("resident_waves_timeline",)}))
 PY

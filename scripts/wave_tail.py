@@ -25,7 +25,7 @@ for p in (ROOT, os.path.join(ROOT, "hello-raytracing_amd"), os.path.join(ROOT, "
 import bench  # noqa: E402
 import hrt  # noqa: E402
 import scenes  # noqa: E402
-from hrt.parallel import rank_params  # noqa: E402
+from hrt.parallel import owned_rows, rank_params  # noqa: E402
 
 
 def summarise(tr: np.ndarray) -> dict:
@@ -37,6 +37,7 @@ def summarise(tr: np.ndarray) -> dict:
     clk0, clk1, w6, w7 = (tr[ok, k].astype(np.int64) for k in (4, 5, 6, 7))
     dclk, jclk = w6 & 0xFFFFFFFF, w6 >> 32  # shader-clock ticks from start to the drain / to the last job take
     last_job = (tr[ok, 2].astype(np.uint64) >> np.uint64(40)).astype(np.int64)  # k_trace: when the last job was taken
+    xcc = (tr[ok, 2] >> 32) & 0xFF
     t0 = st.min()
     span = (en.max() - t0) / 1e5
     pct = lambda a: [round(float(np.percentile(a, q)), 3) for q in (0, 10, 50, 90, 100)]  # noqa: E731
@@ -72,6 +73,12 @@ def summarise(tr: np.ndarray) -> dict:
         if last_job.any() and (dclk > 0).any() else None,
         "clk_per_round_overall_pcts": pct((clk1 - clk0) / np.maximum(w7 >> 48, 1)) if last_job.any() else None,
         "resident_waves_timeline": conc,
+        # per XCD (XCC_ID): end time and the last job's length (k_trace), p50 / p100
+        "by_xcd": {int(x): {"end_ms": [round(float(np.percentile((en - t0)[xcc == x] / 1e5, q)), 3) for q in (50, 100)],
+                            "last_job_to_end_ms": [round(float(np.percentile((en - st - last_job)[xcc == x] / 1e5, q)), 3)
+                                                   for q in (50, 100)] if last_job.any() else None,
+                            "waves": int((xcc == x).sum())}
+                   for x in np.unique(xcc)},
     }
 
 
@@ -95,7 +102,41 @@ def draw(sd, params: dict):
     out = {"kernel": st.kernel.decode(), "trace_ms": round(st.trace_ms, 3), "kernel_ms": round(st.kernel_ms, 3),
            "wall_ms": round(wall * 1e3, 3), "trace_launches": st.trace_launches, "rays": st.queries}
     out.update(summarise(tr))
+    if out.get("jobs_total"):  # k_trace: per-job records after the wave records (renderer.cpp, job_trace)
+        p = r.params
+        nrows = len(owned_rows(p.row0, p.row_step, sd.height, p.row_block))
+        wave_words = 8 * max(((sd.width + 15) // 16) * ((nrows + 15) // 16) * 4, 32 * 256)
+        tiles_w, tiles = (sd.width + 7) // 8, ((sd.width + 7) // 8) * ((nrows + 7) // 8)
+        nj = out["jobs_total"]
+        jb = (C.c_uint64 * (wave_words + nj))()
+        hrt._lib.check(hrt.lib().rt_get_wave_trace(r._h, jb, wave_words + nj), "rt_get_wave_trace")
+        jt = np.frombuffer(jb, dtype=np.uint64)[wave_words:].astype(np.int64)
+        out["jobs"] = summarise_jobs(jt, tiles_w, tiles, nj // tiles, tr)
     return out
+
+
+def summarise_jobs(jt: np.ndarray, tiles_w: int, tiles: int, nchunks: int, tr: np.ndarray) -> dict:
+    """Each job's duration (take to the wave's next take or drain) against when it was taken and where its tile is."""
+    ok = jt != 0
+    dur = (jt & 0xFFFFFFFF)[ok] / 1e5  # ms
+    t0 = tr[:, 0][tr[:, 1] > 0].min() & 0xFFFFFFFF
+    at = (((jt >> 32) - t0) % (1 << 32))[ok] / 1e5
+    job = np.nonzero(ok)[0]
+    row = (job // max(nchunks, 1)) // tiles_w  # tile row
+    pct = lambda a: [round(float(np.percentile(a, q)), 3) for q in (10, 50, 90, 99)] if len(a) else None  # noqa: E731
+    edges = np.percentile(at, [0, 50, 80, 90, 95, 98, 100])
+    by_time = {f"{edges[k]:.2f}-{edges[k + 1]:.2f} ms": pct(dur[(at >= edges[k]) & (at <= edges[k + 1])])
+               for k in range(len(edges) - 1)}
+    rows = np.unique(row)
+    groups = np.array_split(rows, min(10, len(rows)))
+    by_row = {f"tile rows {g[0]}-{g[-1]}": pct(dur[np.isin(row, g)]) for g in groups}
+    late = at >= edges[-3]  # the last 5 % of takes
+    late_rows = np.unique(row[late])
+    same_rows_early = np.isin(row, late_rows) & ~late
+    return {"recorded": int(ok.sum()), "duration_ms_pcts_by_take_time": by_time, "duration_ms_pcts_by_tile_row": by_row,
+            "last_5pct_takes": {"tile_rows": [int(late_rows.min()), int(late_rows.max())] if late.any() else None,
+                                "duration_ms_pcts": pct(dur[late]),
+                                "same_rows_taken_earlier_ms_pcts": pct(dur[same_rows_early])}}
 
 
 def main() -> None:

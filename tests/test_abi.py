@@ -146,3 +146,20 @@ def test_abi_version_guard():
     assert hrt.lib().rt_abi_version(C.byref(v), C.byref(pb), C.byref(sb)) == 0
     assert (v.value, pb.value, sb.value) == (want, C.sizeof(hrt.RtParams), C.sizeof(hrt.RtStats))
     assert hrt.lib().rt_abi_version(None, None, None) == 0
+
+
+def test_hip_runtime_choice_follows_the_soname():
+    """lib() preloads torch's HIP runtime only when its SONAME is the one libhrt.so needs, and says which
+    runtime it chose; the ELF reader it uses sees libhrt.so's DT_NEEDED."""
+    needed = _lib.elf_dynamic_names(_lib.LIB_PATH, 1)
+    assert any(n.startswith("libamdhip64.so") for n in needed), needed
+    hrt.lib()
+    choice = _lib.HIP_RUNTIME_CHOICE
+    trt = _lib._torch_hip_runtime()
+    if trt is None:
+        assert choice["path"] is None and "torch not installed" in choice["reason"]
+    elif _lib.elf_dynamic_names(trt, 14) == [n for n in needed if n.startswith("libamdhip64")]:
+        assert choice["path"] == str(trt) and "preloaded" in choice["reason"]
+    else:
+        assert choice["path"] is None and "does not match" in choice["reason"]
+    assert len(_lib.hip_runtimes()) <= 1
