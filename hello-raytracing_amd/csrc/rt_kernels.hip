@@ -2064,10 +2064,6 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             } else {
                 if (!job_acquire(J, lane, drained, B.job_tile, B.job_f0, B.job_nf)) break;
                 B.blk_f = 0;
-#ifdef HRT_TAIL_PRIO  // (experiment: a wave holding one of the launch's last jobs issues ahead of the others)
-                if (B.job_tile + P.nwaves / max(P.nchunks, 1u) >= P.tiles_w * P.tiles_h)  // (raster order: full images)
-                    __builtin_amdgcn_s_setprio(3);
-#endif
 #ifdef HRT_STAMPS
                 {
                     const unsigned long long now = hrt_realtime();
