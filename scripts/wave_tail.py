@@ -73,6 +73,12 @@ def summarise(tr: np.ndarray) -> dict:
         if last_job.any() and (dclk > 0).any() else None,
         "clk_per_round_overall_pcts": pct((clk1 - clk0) / np.maximum(w7 >> 48, 1)) if last_job.any() else None,
         "resident_waves_timeline": conc,
+        # by dispatch order (wave index deciles: the first-dispatched waves are the oldest on their SIMD), p50 of the last
+        # job's length (k_trace), of the jobs taken and of the end time
+        "by_dispatch_decile": [{"last_job_to_end_ms_p50": round(float(np.median((en - st - last_job)[g] / 1e5)), 3)
+                                if last_job.any() else None,
+                                "jobs_p50": float(np.median(blocks[g])), "end_ms_p50": round(float(np.median((en - t0)[g] / 1e5)), 3)}
+                               for g in np.array_split(np.arange(len(st)), 10)],
         # per XCD (XCC_ID): end time and the last job's length (k_trace), p50 / p100
         "by_xcd": {int(x): {"end_ms": [round(float(np.percentile((en - t0)[xcc == x] / 1e5, q)), 3) for q in (50, 100)],
                             "last_job_to_end_ms": [round(float(np.percentile((en - st - last_job)[xcc == x] / 1e5, q)), 3)
