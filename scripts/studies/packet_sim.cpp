@@ -249,7 +249,7 @@ int main(int argc, char** argv) {
         if (tm[0] == MODE_TRIS) sc.nslots = 0;
     }
     const bool heap = tm[0] != MODE_SPHERE;
-    double hp = 0, hs = 0, nhp = 0, nhs = 0, hu = 0, hul = 0;
+    double hp = 0, hs = 0, nhp = 0, nhs = 0, hu = 0, hul = 0, rc_hit = 0, rc_cull = 0, rc_steps = 0;
     const uint32_t tw = (W + 7) / 8, th = (H + 7) / 8;
     Stats prim, sec;
     Packet pk[3];
@@ -280,7 +280,25 @@ int main(int argc, char** argv) {
                 ray_t cur = r;
                 for (uint32_t b = 0; b < B; b++) {
                     if (sc.nslots) lane_walk(&sc, cur.o, cur.d, b == 0 ? prim : sec);
-                    if (heap) (b == 0 ? hp : hs) += heap_lane(&sc, cur.o, cur.d), (b == 0 ? nhp : nhs) += 1;
+                    if (heap) {
+                        const double st = heap_lane(&sc, cur.o, cur.d);
+                        (b == 0 ? hp : hs) += st, (b == 0 ? nhp : nhs) += 1;
+                        // root cull (mixed program): the mesh's root box entered beyond the sphere winner's t
+                        if (sc.nslots) {
+                            hit_t hs0 = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, FLT_MAX_REF, 0, 0};
+                            closest_sphere(&sc, cur, &hs0);
+                            v3 inv = V(1.0f / cur.d.x, 1.0f / cur.d.y, 1.0f / cur.d.z);
+                            const o_node* nd = &sc.nodes[1];
+                            float t0x = (nd->bmin[0] - cur.o.x) * inv.x, t1x = (nd->bmax[0] - cur.o.x) * inv.x;
+                            float t0y = (nd->bmin[1] - cur.o.y) * inv.y, t1y = (nd->bmax[1] - cur.o.y) * inv.y;
+                            float t0z = (nd->bmin[2] - cur.o.z) * inv.z, t1z = (nd->bmax[2] - cur.o.z) * inv.z;
+                            float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+                            float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+                            const bool root_hit = tmin <= tmax && tmax >= 0.0f;
+                            if (root_hit) rc_hit++;
+                            if (root_hit && tmin > hs0.t * 1.001f) rc_cull++, rc_steps += st;
+                        }
+                    }
                     hit_t h = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, FLT_MAX_REF, 0, 0};
                     if (sc.mode != MODE_TRIS) closest_sphere(&sc, cur, &h);
                     if (heap) {
@@ -307,6 +325,10 @@ int main(int argc, char** argv) {
                "\"rpp\": %.3f, \"hu\": %.4f, \"hul\": %.3f}\n",
                hp / nhp, hs / nhs, nhp / (nhp + nhs), nrays_pk / npk, hu / npk, hul / hu, hp / nhp, hs / nhs, nhp / (nhp + nhs),
                nrays_pk / npk, hu / npk, hul / hu);
+    if (heap && sc.nslots)
+        printf("root cull: queries %.0f, root box hit %.0f (%.3f), culled (entry > sphere t x 1.001) %.0f (%.3f of queries); "
+               "heap steps they take %.0f = %.3f of all heap steps\n",
+               nhp + nhs, rc_hit, rc_hit / (nhp + nhs), rc_cull, rc_cull / (nhp + nhs), rc_steps, rc_steps / (hp + hs));
     if (!sc.nslots) return 0;
     const double qall = prim.q + sec.q;
     printf("queries %.0f (primary %.0f = %.3f)\n", qall, prim.q, prim.q / qall);
