@@ -485,7 +485,8 @@ def main() -> int:
     ap.add_argument("--queue-budget-mb", type=int, default=None,
                     help="sample queue: colour-buffer budget per chunk in MiB (default: the library's)")
     ap.add_argument("--fold", type=int, default=None,
-                    help="sample queue colour fold: 0 auto, 1 sample buffer + k_accumulate, 2 fold ring")
+                    help="sample queue colour fold: 0 auto, 1 sample buffer + k_accumulate, 2 fold ring, 3 two sample "
+                         "buffers, each launch folded by the next")
     ap.add_argument("--heap-lds", type=int, default=None,
                     help="triangle / mixed programs: 0 auto (heap top in LDS when it fits), 1 off")
     ap.add_argument("--steal", type=int, default=None,
@@ -652,7 +653,7 @@ def main() -> int:
         executed = executed_flop_per_launch / (avg_launch_ms * 1e-3) / 1e12
         px = local_rows * sd.width
         if schedule == 2:  # one colour per sample (12 B; 16 B through the fold ring); the spheres read once
-            per_sample = 16.0 if st_last.fold_ring else 12.0
+            per_sample = 16.0 if st_last.fold_ring == 1 else 12.0
             alg_bytes = per_sample * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
         else:  # k_render reads and writes the framebuffer once per launch
             alg_bytes = 24.0 * px + 64.0 * nslots
@@ -689,9 +690,11 @@ def main() -> int:
                 "rays_per_sample": round(total_q / args.steps / (sd.width * sd.height * sd.frames), 4),
                 "parallelism": f"rows{world}",
                 "row_block": args.row_block,
-                # how the sample queue folded the colours in frame order (rt_params.queue_budget_mb):
-                # "sample-buffer" (+ k_accumulate) or the bounded-memory "fold-ring"; device bytes it used
-                "fold": ("fold-ring" if st_last.fold_ring else "sample-buffer") if schedule == 2 else "in-register",
+                # how the sample queue folded the colours in frame order (rt_params.queue_budget_mb, fold):
+                # "sample-buffer" (+ k_accumulate), "sample-buffers-folded-by-next-launch" (two buffers, each launch
+                # folds the one before, k_accumulate the last) or the bounded-memory "fold-ring"; device bytes it used
+                "fold": (["sample-buffer", "fold-ring", "sample-buffers-folded-by-next-launch"][st_last.fold_ring]
+                         if schedule == 2 else "in-register"),
                 "fold_bytes": int(st_last.fold_bytes) if schedule == 2 else 0,
                 # frames per trace launch (the sample buffer's balanced launches, rt_params.queue_budget_mb)
                 "launch_frames": int(st_last.launch_frames) if schedule == 2 else 0,

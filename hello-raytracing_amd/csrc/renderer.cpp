@@ -182,6 +182,8 @@ struct rt_renderer {
     DevBuf<unsigned long long> queues;       // sample buffer: the per-XCD job counters (rt_kernels.hip queue_take_lane0)
     uint32_t cus = 0;                        // compute units of the renderer's device
     DevBuf<float> samples;      // sample-queue colour buffer (frames x tiles x 64 px x 3), tile-major (ring_mode 0)
+    DevBuf<float> samples2;     // the odd launches' buffer when each launch folds the one before (rt_params.fold 3)
+    bool last_fold_next = false;
     DevBuf<float4> ring;        // sample-queue fold ring: job slots x job_frames x 64 px (rgb, unused) (ring_mode 1)
     DevBuf<uint32_t> ring_ctl;  // zeroed per launch: tile fold words (2 words per tile), the free queue (4 per
                                 // slot) and its tail (4); then the job -> slot map
@@ -219,7 +221,7 @@ struct rt_renderer {
         return image.bytes() + sph_geo.bytes() + sph_aux.bytes() + sph_pairs.bytes() + bvh_nodes.bytes() + bvh_sph.bytes() +
                bvh_hnodes.bytes() + bvh_slot.bytes() + bvh_large.bytes() + nodes.bytes() + nodes_so.bytes() + tris.bytes() +
                tri_geo.bytes() + mats.bytes() +
-               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + count_spread.bytes() + samples.bytes() + ring.bytes() + ring_ctl.bytes() +
+               tb_hnodes.bytes() + tb_order.bytes() + counter.bytes() + count_spread.bytes() + samples.bytes() + samples2.bytes() + ring.bytes() + ring_ctl.bytes() +
                wave_trace.bytes() + steal_slots.bytes() + queues.bytes() + tile_cost.bytes() + tile_sum.bytes() + tile_order.bytes() +
                order_scratch.bytes();
     }
@@ -643,7 +645,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         }
         uint32_t chunk = balanced(budget / frame_bytes), log2s = 0;
         P.ring_mode = chunk < std::min(nframes_all, 320u) ? 1u : 0u;
-        if (r->params.fold == RT_FOLD_BUFFER) P.ring_mode = 0u;  // forced (measurements, tests)
+        if (r->params.fold == RT_FOLD_BUFFER || r->params.fold == RT_FOLD_NEXT) P.ring_mode = 0u;  // forced (measurements, tests)
         if (r->params.fold == RT_FOLD_RING) P.ring_mode = 1u;
         const size_t fail_above = (size_t)r->test_fail_alloc_above_mb << 20;
         size_t zero_words = 0;
@@ -737,16 +739,49 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
 #endif
         constexpr size_t QWORDS = (size_t)hrt_dev::NQ * hrt_dev::QSTRIDE;
         P.queues = nullptr;
-        if (HRT_NQ && !P.ring_mode) {
-            rc = ensure(r->queues, QWORDS);
+        if (!P.ring_mode) {  // (+ the fold counter, below)
+            rc = ensure(r->queues, QWORDS + hrt_dev::QSTRIDE);
             if (rc) return rc;
         }
+        // Each launch folds the one before (rt_params.fold 3; rt_kernels.hip fold_prev_tiles): two sample buffers, launch
+        // k writes buffer k % 2 while every FOLD_WAVE_MOD-th wave first folds buffer (k - 1) % 2 into the image;
+        // k_accumulate folds the last launch only. The suspendable-walk kernels, draws of two or more launches; auto with
+        // the automatic colour budget (it doubles the colour memory: C3 17.5 GB). C3 38.38 -> 38.76-38.83 Grays/s with 1 in
+        // 32 / 64 / 128 waves folding, 38.62-38.65 with 1 in 16, 38.30-38.44 with 1 in 1 or 4; C5 +0.2 %
+        // (profiles/r06/fold_next/).
+        constexpr uint32_t FOLD_WAVE_MOD = 64;
+        bool fold_next = !P.ring_mode && split && count > chunk &&
+                         (r->params.fold == RT_FOLD_NEXT || (r->params.fold == RT_FOLD_AUTO && r->params.queue_budget_mb == 0u));
+        if (fold_next) {
+            rc = ensure_within(r->samples2, (size_t)chunk * frame_floats, std::max(budget, frame_bytes), fail_above);
+            if (rc == RT_ERR_ALLOC) {
+                (void)hipGetLastError();
+                fold_next = false;
+            } else if (rc) {
+                return rc;
+            }
+        }
+        if (!fold_next) r->samples2.release();
+        else r->fold_bytes *= 2u;
+        r->last_fold_next = fold_next;
         // (suspend_below 0: the same kernels with a threshold no wave reaches, 1 walking lane: no suspension)
         P.suspend_below = split ? std::max(r->params.suspend_below, 1u) : 0u;
         r->last_suspend = split ? r->params.suspend_below : 0u;
         P.job_frames = jf;
         HIP_TRY(hipEventRecord(r->ev_start, r->stream));
-        for (uint32_t done = 0; done < count; done += chunk) {
+        P.fold_prev = nullptr;
+        for (uint32_t done = 0, k = 0; done < count; done += chunk, k++) {
+            if (fold_next) {
+                P.samples = (k & 1u) ? r->samples2.ptr : r->samples.ptr;
+                if (k > 0u) {  // the launch before: its buffer, frames and first frame
+                    P.fold_prev = (k & 1u) ? r->samples.ptr : r->samples2.ptr;
+                    P.fold_nframes = P.nframes;
+                    P.fold_frame0 = P.frame0;
+                    P.fold_next = (uint32_t*)(r->queues.ptr + QWORDS);
+                    P.fold_mod = FOLD_WAVE_MOD;
+                    HIP_TRY(hipMemsetAsync(P.fold_next, 0, sizeof(uint32_t), r->stream));
+                }
+            }
             P.nframes = std::min(chunk, count - done);
             P.time0 = time0 + done * dtime;
             P.frame0 = r->frame_count + done;
@@ -819,7 +854,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
                 r->order_tiles = ntiles;
                 r->cost_learn = false;
             }
-            if (!P.ring_mode) {
+            if (!P.ring_mode && (!fold_next || done + chunk >= count)) {
                 HIP_TRY(hrt_launch_accumulate(P, r->stream));
                 launches++;
             }
@@ -848,7 +883,7 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
     r->stats.local_rows = P.nrows;
     std::snprintf(r->stats.kernel, sizeof r->stats.kernel, "%s", hrt_last_kernel());
     if (schedule == RT_SCHEDULE_QUEUE && count && P.nrows) {
-        r->stats.fold_ring = P.ring_mode;
+        r->stats.fold_ring = P.ring_mode ? 1u : r->last_fold_next ? 2u : 0u;
         r->stats.fold_bytes = r->fold_bytes;
         r->stats.launch_frames = std::min(count, r->last_launch_frames);
         r->stats.ordered_launches = r->last_ordered;
@@ -945,6 +980,7 @@ void delete_buffers(rt_renderer* r) {
     r->steal_slots.release();
     r->queues.release();
     r->samples.release();
+    r->samples2.release();
     r->ring.release();
     r->ring_ctl.release();
     r->wave_trace.release();
@@ -1067,7 +1103,8 @@ int rt_set_params(rt_renderer* r, const rt_params* p) {
     if (p->schedule > RT_SCHEDULE_QUEUE) return fail(RT_ERR_ARG, "rt_set_params: unknown schedule");
     if (p->tri_bvh > 1) return fail(RT_ERR_ARG, "rt_set_params: tri_bvh must be 0 or 1");
     if (p->suspend_below > 64) return fail(RT_ERR_ARG, "rt_set_params: suspend_below must be 0..64");
-    if (p->fold > RT_FOLD_RING) return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer or 2 ring");
+    if (p->fold > RT_FOLD_NEXT)
+        return fail(RT_ERR_ARG, "rt_set_params: fold must be 0 auto, 1 buffer, 2 ring or 3 buffers folded by the next launch");
     if (p->heap_lds > 2) return fail(RT_ERR_ARG, "rt_set_params: heap_lds must be 0 auto, 1 off or 2 on");
     if (p->steal > 2) return fail(RT_ERR_ARG, "rt_set_params: steal must be 0 auto, 1 off or 2 on");
     if (p->tail_split > 3) return fail(RT_ERR_ARG, "rt_set_params: tail_split must be 0 auto, 1 off, 2 quarters or 3 eighths");
@@ -1306,6 +1343,7 @@ int rt_release_scratch(rt_renderer* r) {
     }
     HIP_TRY(hipStreamSynchronize(r->stream));
     r->samples.release();
+    r->samples2.release();
     r->ring.release();
     r->ring_ctl.release();
     return RT_OK;

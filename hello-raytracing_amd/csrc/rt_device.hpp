@@ -198,6 +198,11 @@ struct KParams {
     uint32_t* tile_cost;
     const uint32_t* tile_order;
     unsigned long long* count_spread;  // CSPREAD x CSTRIDE words: the work counters' copies
+    // fold of the previous launch's sample buffer inside this launch (rt_kernels.hip fold_prev_tiles; null: none):
+    // every fold_mod-th wave folds tiles taken from *fold_next before it traces
+    const float* fold_prev;
+    uint32_t* fold_next;
+    uint32_t fold_nframes, fold_frame0, fold_mod, pad_f;
 };
 
 // KParams in the kernarg segment (constant address space: scalar loads), as a pointer the compiler cannot

@@ -1640,6 +1640,31 @@ __device__ __forceinline__ void fold_pixel(float* px, const float* tile, uint32_
     px[2] = acc2;
 }
 
+// The previous launch's sample buffer folded inside this launch (rt_params.fold 3, RT_FOLD_NEXT; renderer.cpp: two
+// sample buffers): every fold_mod-th wave takes tiles from a counter and folds each like k_accumulate before it starts
+// tracing, so the fold's HBM reads run beside the other waves' tracing instead of in a launch of their own between two
+// trace launches (the persistent grid holds every wave slot: a k_accumulate on a second stream only trickles in; DESIGN.md
+// §6 Round 6). The folds stay in frame order: launch k's buffer is folded inside launch k + 1, before launch k + 1's own
+// buffer is folded. The suspendable-walk kernels only (k_trace_split, k_trace_split_tris: their register allocation is
+// unchanged by it; k_trace's loses a wave).
+__device__ __forceinline__ void fold_prev_tiles(const KParams& P, uint32_t lane) {
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave % P.fold_mod != 0u) return;
+    const uint32_t ntiles = P.tiles_w * P.tiles_h;
+    const size_t npad3 = (size_t)ntiles * 192u;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0u) t = __hip_atomic_fetch_add(P.fold_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= ntiles) break;
+        const uint32_t x = (t % P.tiles_w) * 8u + (lane & 7u);
+        const uint32_t kr = (t / P.tiles_w) * 8u + (lane >> 3);
+        if (x < P.W && kr < P.nrows)
+            fold_pixel<8>(P.image + ((size_t)kr * P.W + x) * 3u, P.fold_prev + (size_t)t * 192u, lane * 3u, npad3,
+                          P.fold_nframes, P.fold_frame0, P.ema_cap);
+    }
+}
+
 #ifdef HRT_RINGSTAT
 // diagnostic build: per-wave ring statistics (stall rounds: every entry busy; slot-wait rounds; folds; fold
 // cycles / 16), summed into counter[5..8] at wave exit
@@ -2738,6 +2763,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
     uint32_t job_tile = 0, job_f0 = 0, job_nf = 0, blk_f = 0, blk_next = 64;  // wave-uniform
     __shared__ uint32_t wjobs[4 * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
+    if (P.fold_prev != nullptr) fold_prev_tiles(P, lane);
     HRT_PHASE_DECL;
 #ifdef HRT_STAMPS
     WaveRecord wrec;
@@ -3041,6 +3067,7 @@ k_trace_split_tris(const KParams P) {
     BlockState B;
     __shared__ uint32_t wjobs[(WGT / 64u) * WJ_WORDS];
     const WaveJobs J = wave_jobs(wjobs);
+    if (P.fold_prev != nullptr) fold_prev_tiles(P, lane);
     bool drained = false;
     Ray ray;
     f3 att = mk(1.0f, 1.0f, 1.0f);

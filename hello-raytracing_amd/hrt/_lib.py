@@ -27,7 +27,7 @@ RT_MODE_SPHERE = 0
 RT_MODE_TRIS = 1
 RT_MODE_MIXED = 2
 RT_SCHEDULE_AUTO, RT_SCHEDULE_TILES, RT_SCHEDULE_QUEUE = 0, 1, 2
-RT_FOLD_AUTO, RT_FOLD_BUFFER, RT_FOLD_RING = 0, 1, 2
+RT_FOLD_AUTO, RT_FOLD_BUFFER, RT_FOLD_RING, RT_FOLD_NEXT = 0, 1, 2, 3
 
 
 class RtParams(C.Structure):

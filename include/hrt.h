@@ -96,8 +96,13 @@ typedef struct rt_params {
                                   owns rows row0 + k*row_step*row_block + j, j < row_block, in that order.
                                   Rank r of N with row_block 8 and row0 = 8r, row_step = N owns whole
                                   8-row tile rows dealt round-robin (bench.py)            */
-    uint32_t fold;             /* sample queue colour fold: 0 auto (by queue_budget_mb, above), 1 the sample
-                                  buffer + k_accumulate, 2 the fold ring (bounded memory); bit-identical */
+    uint32_t fold;             /* sample queue colour fold: 0 auto (by queue_budget_mb, above; with the automatic
+                                  budget, draws of two or more launches of the suspendable-walk kernels fold as 3),
+                                  1 the sample buffer + k_accumulate after every launch, 2 the fold ring (bounded
+                                  memory), 3 two sample buffers: each launch's waves fold the launch before it (1 in
+                                  64 waves first folds tiles, then traces), k_accumulate the last launch only —
+                                  twice the colour memory of 1 (C3 17.5 GB), C3 +1 %;
+                                  k_trace's draws fold as 1; bit-identical                               */
     uint32_t heap_lds;         /* triangle / mixed programs: the top of the implicit heap in LDS, 0 auto = on,
                                   1 off (every node from L1/L2), 2 on: nodes 1..1023 as sign-ordered nodes
                                   (768-lane workgroups; nodes 1..255 with the deferred sphere scan; heaps of
@@ -136,6 +141,7 @@ typedef struct rt_params {
 #define RT_FOLD_AUTO 0u
 #define RT_FOLD_BUFFER 1u
 #define RT_FOLD_RING 2u
+#define RT_FOLD_NEXT 3u
 
 #define RT_SCHEDULE_AUTO 0u
 #define RT_SCHEDULE_TILES 1u
@@ -163,7 +169,8 @@ typedef struct rt_stats {
                               buffer (frames per launch x pixels x 12 B) or the fold ring (job slots x
                               job_frames x 64 px x 16 B plus control words); 0 for the tiles schedule    */
     uint32_t fold_ring;    /* 1: the last draw folded through the fold ring (bounded memory), 0: through the
-                              sample buffer and k_accumulate (rt_params.queue_budget_mb decides)         */
+                              sample buffer and k_accumulate, 2: through two sample buffers, each launch folded
+                              inside the next (rt_params.fold 3; rt_params.queue_budget_mb decides)        */
     uint32_t launch_frames; /* sample queue: frames per trace launch of the last draw (the last launch may
                               have fewer; rt_params.queue_budget_mb)                                   */
     uint64_t device_bytes; /* device memory the renderer holds after the last draw call (image, scene,

@@ -62,20 +62,23 @@ def test_c3_as_timed_crosses_the_ema_switch_inside_a_launch():
     assert (sd.width, sd.height, sd.frames) == (1920, 1080, 1024)
     r, img, st = timed_draw(sd)
     # the composition of the bench line (kernel, 3 launches of 352 frames per step, all three dealt in the cost order
-    # the warmup step learnt)
-    assert composition(st) == ("k_trace_split<true, false, false, false>", 3, 352, 3, 0), composition(st)
+    # the warmup step learnt, two sample buffers: launches 2 and 3 fold the launch before, k_accumulate the third)
+    assert composition(st) == ("k_trace_split<true, false, false, false>", 3, 352, 3, 2), composition(st)
+    assert st.launches == 4, st.launches
     assert st.box_tests == 0 and st.sphere_tests == 0  # uncounted, as timed
     assert 704 < 1000 < 1024  # frame 1000 is folded by the third launch's k_accumulate
     rows = (7, 536, 3)  # rows 7, 543, 1079
     ref, _ = scenes.oracle_render(sd, rows=rows)
     assert_bits(img[7::536], ref, "C3 timed composition, rows 7 / 543 / 1079 x 1024 frames")
     # the same rows alone, in the same three launches (a 62 MiB budget holds 352 frames of one tile row), give the
-    # oracle's ray count too (stealing off: the bench's kernel)
+    # oracle's ray count too (stealing off: the bench's kernel; each launch folded by the next, as timed)
     r2 = scenes.make_renderer(sd)
-    r2.set_params(row0=7, row_step=536, row_block=1, **bench.timed_knobs(queue_budget_mb=62, steal=1))
+    r2.set_params(row0=7, row_step=536, row_block=1,
+                  **bench.timed_knobs(queue_budget_mb=62, steal=1, fold=hrt.RT_FOLD_NEXT))
     r2.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
     st2 = r2.stats()
     assert st2.kernel.decode() == "k_trace_split<true, false, false, false>" and st2.trace_launches == 3
+    assert st2.fold_ring == 2
     assert st2.launch_frames == 352
     _, q = scenes.oracle_render(sd, rows=rows)
     assert st2.queries == q
@@ -95,15 +98,17 @@ def test_c5_as_timed_in_twelve_launches():
     """C5's full 4K image takes 9 s per step; its timed composition — twelve sample-buffer launches of 342 frames (the
     auto budget's 32 GiB cap), frame 1000 inside the third, the kernel k_trace_split_tris<2, 4, 3, false> — is drawn on
     one row with a 121 MiB budget (the same 342-frame launches) and stealing off (a one-row draw has few jobs per wave,
-    which would turn the auto stealing on). A 512-column window of the row against the oracle at all 4096 frames."""
+    which would turn the auto stealing on), each launch folded by the next as the auto budget's are. A 512-column
+    window of the row against the oracle at all 4096 frames."""
     sd = scenes.config_c5()
     assert (sd.width, sd.height, sd.frames) == (3840, 2160, 4096)
     r = scenes.make_renderer(sd)
-    r.set_params(row0=1080, row_step=2160, row_block=1, **bench.timed_knobs(queue_budget_mb=121, steal=1))
+    r.set_params(row0=1080, row_step=2160, row_block=1,
+                 **bench.timed_knobs(queue_budget_mb=121, steal=1, fold=hrt.RT_FOLD_NEXT))
     r.draw_frames(sd.frames, bench.TIME0, bench.DTIME)
     img, st = r.read_image(), r.stats()
     assert st.kernel.decode() == "k_trace_split_tris<2, 4, 3, false>", st.kernel
-    assert (st.trace_launches, st.launch_frames, st.fold_ring) == (12, 342, 0), (st.trace_launches, st.launch_frames)
+    assert (st.trace_launches, st.launch_frames, st.fold_ring) == (12, 342, 2), composition(st)
     x0, nx = 1664, 512
     ref, _ = scenes.oracle_render(sd, rows=(1080, 1, 1), x0=x0, nx=nx)
     assert_bits(img[:, x0:x0 + nx], ref, "C5 timed composition, row 1080, columns 1664-2175 x 4096 frames")
