@@ -654,6 +654,11 @@ def main() -> int:
         px = local_rows * sd.width
         if schedule == 2:  # one colour per sample (12 B; 16 B through the fold ring); the spheres read once
             per_sample = 16.0 if st_last.fold_ring == 1 else 12.0
+            # (fold 3: launches 2..n also read the launch before's colours, 12 B per sample, and fold them into the
+            # image: on average (n - 1) / n of a launch's colours more per trace launch)
+            tl = max(int(st_last.trace_launches), 1)
+            if st_last.fold_ring == 2:
+                per_sample += 12.0 * (tl - 1) / tl
             alg_bytes = per_sample * px * sd.frames * args.steps / nl + 64.0 * nslots  # + ragged-tile padding
         else:  # k_render reads and writes the framebuffer once per launch
             alg_bytes = 24.0 * px + 64.0 * nslots
