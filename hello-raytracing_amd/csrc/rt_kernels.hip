@@ -1648,8 +1648,11 @@ __device__ __forceinline__ void fold_pixel(float* px, const float* tile, uint32_
 // buffer is folded. The suspendable-walk kernels only (k_trace_split, k_trace_split_tris: their register allocation is
 // unchanged by it; k_trace's loses a wave).
 __device__ __forceinline__ void fold_prev_tiles(const KParams& P, uint32_t lane) {
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wave % P.fold_mod != 0u) return;
+    // Wave 0 of every m-th group of 8 consecutive workgroups (m = fold_mod / waves per workgroup): blocks are dealt to
+    // the 8 XCDs round-robin, so the folders sit on all eight. (Every fold_mod-th wave of the grid would, with 4-wave
+    // workgroups, be wave 0 of every 16th block — all on one XCD: C3 -0.3 %.)
+    const uint32_t m = max(P.fold_mod / (blockDim.x >> 6), 1u);
+    if ((threadIdx.x >> 6) != 0u || (blockIdx.x >> 3) % m != 0u) return;
     const uint32_t ntiles = P.tiles_w * P.tiles_h;
     const size_t npad3 = (size_t)ntiles * 192u;
     for (;;) {
