@@ -749,7 +749,10 @@ int launch_frames(rt_renderer* r, uint32_t count, uint32_t time0, uint32_t dtime
         // the automatic colour budget (it doubles the colour memory: C3 17.5 GB). C3 38.38 -> 38.76-38.83 Grays/s with 1 in
         // 32 / 64 / 128 waves folding, 38.62-38.65 with 1 in 16, 38.30-38.44 with 1 in 1 or 4; C5 +0.2 %
         // (profiles/r06/fold_next/).
-        constexpr uint32_t FOLD_WAVE_MOD = 64;
+#ifndef HRT_FOLD_WAVE_MOD
+#define HRT_FOLD_WAVE_MOD 64
+#endif
+        constexpr uint32_t FOLD_WAVE_MOD = HRT_FOLD_WAVE_MOD;
         bool fold_next = !P.ring_mode && split && count > chunk &&
                          (r->params.fold == RT_FOLD_NEXT || (r->params.fold == RT_FOLD_AUTO && r->params.queue_budget_mb == 0u));
         if (fold_next) {
