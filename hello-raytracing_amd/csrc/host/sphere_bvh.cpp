@@ -48,9 +48,15 @@ struct Builder {
     SphereBvh* out;
     uint32_t max_depth = 0;
     // leaf policy (fixed: the library reads no environment variable; tuned values below)
-    uint32_t max_leaf = BVH_MAX_LEAF;
+#ifndef HRT_BVH_MAX_LEAF
+#define HRT_BVH_MAX_LEAF BVH_MAX_LEAF
+#endif
+#ifndef HRT_BVH_TCOST
+#define HRT_BVH_TCOST 0.5
+#endif
+    uint32_t max_leaf = HRT_BVH_MAX_LEAF;
     uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
-    double traversal_cost = 0.5;
+    double traversal_cost = HRT_BVH_TCOST;
     // binned SAH over all three axes (all_axes false: the widest axis, 16 bins, as first built). C3,
     // Grays/s by bin count: 8 25.9, 16 26.8, 24 26.9, 32 27.7, 48 26.8, 64 28.0 (box / sphere tests per ray
     // 16.0 / 4.5 at 64, 16.8 / 5.4 first); an exact sweep SAH gave 26.9: tree shape matters more than
