@@ -90,6 +90,7 @@ __device__ __forceinline__ int scan_spheres(const KParams& P, const Ray& r, floa
     return scan_spheres_p(&P, r, best);
 }
 
+
 // The reference's t for slot i, recomputed exactly as the scan computes it (scalar IEEE ops give the
 // same bits as the packed lanes). Returns -1 when the reference would give t = -1 (disc < 0).
 __device__ __forceinline__ float exact_sphere_t(const KParams& P, const Ray& r, int i, float a4, float a2) {
@@ -221,6 +222,16 @@ __device__ __forceinline__ float exact_t_geo(const float4 g, const Ray& r, float
     if (!(disc >= 0.0f && b <= 0.0f)) return -1.0f;  // t would be <= 0, NaN or -1: never accepted
     if (FAST) return div_exact(-b - sqrt_exact(disc), a2);
     return (-b - __builtin_sqrtf(disc)) / a2;
+}
+
+// exact_t_geo's own test, alone: true when exact_t_geo goes on to the root (the same operations, so the same verdict)
+__device__ __forceinline__ bool sphere_candidate(const float4 g, const Ray& r, float a4) {
+    const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
+    const float bd = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+    const float b = bd + bd;
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
+    const float disc = __builtin_fmaf(b, b, (-a4) * c);
+    return disc >= 0.0f && b <= 0.0f;
 }
 
 // 1/d for the slab tests, |d| >= 1e-30 (else +-1e30). v_rcp_f32 (1 ulp) by default: the padding budget
@@ -416,6 +427,9 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
 #ifndef HRT_LEAFIV
 #define HRT_LEAFIV 1
 #endif
+#ifndef HRT_LEAF_DEFER
+#define HRT_LEAF_DEFER 1
+#endif
     if constexpr (NOOVF && SO && HRT_BTEST) {
         // The sign-ordered walks without overflow (k_trace_split with LDS nodes, the HL3 mixed kernels) with the
         // descent as a bottom-tested loop: one exit (a miss, or a leaf reached) and the node / stack depth updated
@@ -473,6 +487,41 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                 }
 #endif
                 const uint32_t first = (node >> 4) & 0x07FFFFFFu, cnt = node & 15u;
+#if HRT_LEAF_DEFER
+                if constexpr (SELECT) {
+                    // Two passes over the leaf (k_trace_split): the cheap discriminant test of every sphere first, the
+                    // lane's candidates (disc >= 0 && b <= 0: 13 % of C3's leaf tests) kept as a bit mask; then the exact
+                    // roots of the candidates only. In one pass the root sequence (sqrt, division, the tie check: ~45
+                    // instructions) ran for every sphere of the leaf in which ANY walking lane had a candidate — nearly
+                    // every one, at a few lanes each; now it runs once per candidate of the lane with the most (mostly
+                    // once per leaf). C3 +1.0 % (profiles/r06/leaf_defer/); the mixed kernels' sphere walk (C5, IEEE
+                    // roots inside the begin phase) measured -0.2 % and keeps one pass. Exact: the same spheres are
+                    // tested with the same arithmetic, the (t, slot) minimum does not depend on the order, and bt (the
+                    // boxes' bound) is final before the next box step either way.
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
+                    auto leaf_geo = [&](uint32_t o) -> float4 {
+                        const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
+                        return float4{v.x, v.y, v.z, v.w};
+                    };
+                    uint32_t cand = 0u;
+                    for (uint32_t o = first * 16u, oe = (first + cnt) * 16u, bit = 1u; o != oe; o += 16u, bit <<= 1) {
+                        if (sphere_candidate(leaf_geo(o), r, a4)) cand |= bit;
+                    }
+                    while (cand != 0u) {
+                        const uint32_t o = (first + (uint32_t)__builtin_ctz(cand)) * 16u;
+                        cand &= cand - 1u;
+                        const float t = exact_t_geo<true>(leaf_geo(o), r, a4, a2);
+                        if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
+                            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                                (void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
+                            const int slot = (int)__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)(o >> 2), 0, 0);
+                            if (t < bt || (bc >= 0 && slot < bvh_slot_of(P, bc))) { bt = t; bc = (int)(o >> 4); }
+                        }
+                    }
+                } else
+#endif
 #if HRT_LEAFIV
                 // one induction variable: the sphere's byte offset (slot word at o / 4, BVH position o / 16)
                 for (uint32_t o = first * 16u, oe = (first + cnt) * 16u; o != oe; o += 16u) {
