@@ -494,10 +494,10 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                     // roots of the candidates only. In one pass the root sequence (sqrt, division, the tie check: ~45
                     // instructions) ran for every sphere of the leaf in which ANY walking lane had a candidate — nearly
                     // every one, at a few lanes each; now it runs once per candidate of the lane with the most (mostly
-                    // once per leaf). C3 +1.0 % (profiles/r06/leaf_defer/); the mixed kernels' sphere walk (C5, IEEE
-                    // roots inside the begin phase) measured -0.2 % and keeps one pass. Exact: the same spheres are
-                    // tested with the same arithmetic, the (t, slot) minimum does not depend on the order, and bt (the
-                    // boxes' bound) is final before the next box step either way.
+                    // once per leaf). C3 +1.0 % (profiles/r06/leaf_defer/); the mixed kernels' sphere walk (C5, inside
+                    // the begin phase) keeps one pass: two passes measured -0.2 % with its IEEE roots, -0.25 % with
+                    // these. Exact: the same spheres are tested with the same arithmetic, the (t, slot) minimum does not
+                    // depend on the order, and bt (the boxes' bound) is final before the next box step either way.
                     typedef float f4v __attribute__((ext_vector_type(4)));
                     const __amdgpu_buffer_rsrc_t rs =
                         __builtin_amdgcn_make_buffer_rsrc((void*)P.bvh_sph, (short)0, (int)(P.bvh_nleaf * 16u), 0x00020000);
