@@ -496,7 +496,8 @@ def main() -> int:
                     help="sample queue: 0 auto (the most expensive tiles first for a row partition's shares "
                          "without stealing), 1 off, 2 on")
     ap.add_argument("--packet", type=int, default=None,
-                    help="sphere program: primary rays walked as one packet per frame block: 0 auto (on), 1 off, 2 on")
+                    help="sphere program: primary rays walked as one packet per frame block: 0 auto (off: -8 %% on C3), 1 off, "
+                         "2 on")
     ap.add_argument("--tri-bvh", type=int, default=0,
                     help="triangle program: 0 the reference heap walk (parity), 1 opt-in SAH tree (non-parity)")
     ap.add_argument("--variant", type=int, default=0,

@@ -55,7 +55,10 @@ struct Builder {
 #define HRT_BVH_TCOST 0.5
 #endif
     uint32_t max_leaf = HRT_BVH_MAX_LEAF;
-    uint32_t leaf_depth = 0;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
+#ifndef HRT_BVH_LEAF_DEPTH
+#define HRT_BVH_LEAF_DEPTH 0
+#endif
+    uint32_t leaf_depth = HRT_BVH_LEAF_DEPTH;  // any subtree of <= max_leaf spheres becomes a leaf (measured best on C3)
     double traversal_cost = HRT_BVH_TCOST;
     // binned SAH over all three axes (all_axes false: the widest axis, 16 bins, as first built). C3,
     // Grays/s by bin count: 8 25.9, 16 26.8, 24 26.9, 32 27.7, 48 26.8, 64 28.0 (box / sphere tests per ray
