@@ -799,6 +799,15 @@ def _random_scene(kind: str, seed: int):
         for _ in range(64):
             c = rng.uniform([-3, -1, -8], [3, 2, -3]) + off
             o.append(mats[rng.integers(3)](hrt.Vec3(*c), float(rng.uniform(0.1, 0.6))))
+    elif kind == "nested_clusters":  # the two-pass leaf: several candidates per lane in one leaf, exact ties
+        for _ in range(24):
+            c = rng.uniform([-3, 0, -8], [3, 2, -3])
+            rad = float(rng.uniform(0.2, 0.5))
+            dup = mats[rng.integers(3)](hrt.Vec3(*c), rad)
+            o.append(dup)                                                  # outer sphere
+            o.append(mats[rng.integers(3)](hrt.Vec3(*c), 0.7 * rad))       # concentric inner
+            o.append(mats[rng.integers(3)](hrt.Vec3(*(c + [0.3 * rad, 0, 0])), 0.5 * rad))  # overlapping
+            o.append(dup)                                                  # the outer one again: a t tie, higher slot
     o.append(hrt.Sphere.new_lambertian(hrt.Vec3(*(np.array([0.0, -1000.5, -5.0]) + off)), 1000.0,
                                        hrt.Vec3(0.5, 0.5, 0.5)))
     cam = hrt.Camera.new(hrt.Vec3(*(np.array([0.5, 2.0, 3.0]) + off)), hrt.Vec3(*(np.array([0.0, 0.0, -5.0]) + off)),
@@ -808,7 +817,7 @@ def _random_scene(kind: str, seed: int):
 
 
 @pytest.mark.parametrize("schedule", [1, 2])
-@pytest.mark.parametrize("kind", ["tangent_grid", "radius_spread", "far_offset"])
+@pytest.mark.parametrize("kind", ["tangent_grid", "radius_spread", "far_offset", "nested_clusters"])
 def test_culling_bvh_exact_on_adversarial_scenes(kind, schedule):
     """Tiles (k_render) and the sample queue (k_trace_split; nodes in LDS: these trees have < 192 nodes)."""
     sd = _random_scene(kind, 7)
