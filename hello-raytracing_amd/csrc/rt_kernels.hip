@@ -468,7 +468,13 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                     const uint32_t near = lfirst ? c0.w : c1.w, far = lfirst ? c1.w : c0.w;
                     const bool both = hl && hr;
                     any = hl || hr;
-                    if (both) stack[sp * LS] = far;
+#ifndef HRT_PUSH_ALWAYS
+#define HRT_PUSH_ALWAYS 1
+#endif
+                    // (HRT_PUSH_ALWAYS: the far child is written whether or not it is pushed — one slot past the top
+                    // when it is not, never read since sp does not advance, and inside the stack: a box step runs at a
+                    // node of depth d <= depth - 1 with sp <= d — so the store needs no branch and exec-mask save)
+                    if (HRT_PUSH_ALWAYS || both) stack[sp * LS] = far;
                     sp += both ? 1 : 0;
                     node = any ? near : node;
                 } while (any && !(node & BVH_LEAF_BIT));
