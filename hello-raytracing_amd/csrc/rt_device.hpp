@@ -316,6 +316,30 @@ __device__ __forceinline__ f3 normalize_exact(f3 a) {
     return normalize(a);
 }
 
+// The guarded sequences above with their range guard as ONE wave-uniform branch (k_trace_split's shading): the fast
+// sequence runs for every lane, and only a wave with a lane outside its range recomputes that lane with the guarded
+// function itself. The same bits; in the common case a compare and a scalar branch instead of an exec-mask save, a
+// branch and a restore around each arm.
+__device__ __forceinline__ float sqrt_exact_u(float x) {
+    float s = sqrt_rn_mid(x);
+    const bool slow = !(x >= 0x1p-100f && x <= 0x1p100f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) s = __builtin_sqrtf(x);
+    }
+    return s;
+}
+__device__ __forceinline__ f3 normalize_exact_u(f3 a) {
+    const float lo = fmin_ieee(fmin_ieee(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    const float hi = fmax_ieee(fmax_ieee(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    const RcpRN d = rcp_rn_setup(sqrt_rn_mid(dot(a, a)));
+    f3 q = mk(div_rn_mid(a.x, d), div_rn_mid(a.y, d), div_rn_mid(a.z, d));
+    const bool slow = !(lo >= 0x1p-40f && hi <= 0x1p40f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) q = normalize(a);
+    }
+    return q;
+}
+
 // PCG hash step — shader_sphere.wgsl:87-93.
 __device__ __forceinline__ uint32_t pcg_next(uint32_t s) {
     uint32_t old = s + 747796405u + 2891336453u;
@@ -330,14 +354,15 @@ __device__ __forceinline__ float rng_float(uint32_t& s) {
 
 // reflect / refract / reflectance — shader_sphere.wgsl:156-171.
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - (2.0f * dot(v, n)) * n; }
-// FAST: the range-guarded exact square roots (sphere program); else the IEEE ones (the same bits).
-template <bool FAST = true>
+// FAST: the range-guarded exact square roots (sphere program); else the IEEE ones (the same bits). U: their guards as
+// wave-uniform branches (sqrt_exact_u).
+template <bool FAST = true, bool U = false>
 __device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {
     float cos_t = fmin_ieee(dot(-uv, n), 1.0f);
     f3 perp = e * (uv + cos_t * n);
-    float len = FAST ? sqrt_exact(dot(perp, perp)) : length(perp);
+    float len = FAST ? (U ? sqrt_exact_u(dot(perp, perp)) : sqrt_exact(dot(perp, perp))) : length(perp);
     const float q = __builtin_fabsf(1.0f - len * len);
-    f3 par = (-(FAST ? sqrt_exact(q) : __builtin_sqrtf(q))) * n;
+    f3 par = (-(FAST ? (U ? sqrt_exact_u(q) : sqrt_exact(q)) : __builtin_sqrtf(q))) * n;
     return perp + par;
 }
 __device__ __forceinline__ float reflectance(float cosine, float ref_idx) {

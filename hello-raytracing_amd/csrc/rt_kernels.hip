@@ -234,6 +234,28 @@ __device__ __forceinline__ bool sphere_candidate(const float4 g, const Ray& r, f
     return disc >= 0.0f && b <= 0.0f;
 }
 
+// exact_t_geo<true> of a sphere sphere_candidate accepted (disc >= 0, b <= 0: its test is not repeated), with the
+// range guards of sqrt_exact / div_exact as one wave-uniform branch: the fast sequences run for every lane, and only a
+// wave with a lane outside their ranges (disc outside [2^-100, 2^100], a numerator or 2a outside [2^-60, 2^60], a zero
+// numerator) recomputes those lanes with exact_t_geo's own operations. The same bits as exact_t_geo<true>.
+// (need false: the lane's result is discarded — it takes no fallback)
+__device__ __forceinline__ float candidate_t(const float4 g, const Ray& r, float a4, float a2, bool need = true) {
+    const float ocx = r.o.x - g.x, ocy = r.o.y - g.y, ocz = r.o.z - g.z;
+    const float bd = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+    const float b = bd + bd;
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - g.w;
+    const float disc = __builtin_fmaf(b, b, (-a4) * c);
+    const float num = -b - sqrt_rn_mid(disc);
+    float t = div_rn_mid(num, rcp_rn_setup(a2));
+    const float an = __builtin_fabsf(num);
+    const bool slow = need && !(disc >= 0x1p-100f && disc <= 0x1p100f && an >= 0x1p-60f && an <= 0x1p60f &&
+                                a2 >= 0x1p-60f && a2 <= 0x1p60f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) t = div_exact(-b - sqrt_exact(disc), a2);
+    }
+    return t;
+}
+
 // 1/d for the slab tests, |d| >= 1e-30 (else +-1e30). v_rcp_f32 (1 ulp) by default: the padding budget
 // covers it (DESIGN.md §Sphere BVH exactness, slab arithmetic).
 __device__ __forceinline__ float robust_inv(float d) {
@@ -321,9 +343,20 @@ __device__ __forceinline__ bool bvh_begin(const KParams& P, const Ray& r, float 
     float bt = best;
     int bc = -1;
     const uint32_t nlarge = KA ? kargs()->nlarge : P.nlarge;  // (KA: loaded per query, not held in SGPRs)
+#ifndef HRT_CAND_T
+#define HRT_CAND_T 2
+#endif
     for (uint32_t k = 0; k < nlarge; k++) {  // ascending slots: a later equal t never wins here
         const int i = P.large_slots[k];
-        const float t = exact_t_geo<FAST>(P.sph_geo[i], r, a4, a2);
+        float t;
+        if constexpr (FAST && HRT_CAND_T >= 2) {  // (the root for every lane, selected by the test: no branch around it)
+            const float4 g = P.sph_geo[i];
+            const bool cand = sphere_candidate(g, r, a4);
+            t = candidate_t(g, r, a4, a2, cand);
+            t = cand ? t : -1.0f;
+        } else {
+            t = exact_t_geo<FAST>(P.sph_geo[i], r, a4, a2);
+        }
         if (beats(t, i, bt, bc >= 0 ? bvh_slot_of(P, bc) : -1)) { bt = t; bc = (int)(nleaf + k); }
     }
     if constexpr (COUNT) tally.spheres += nlarge;
@@ -518,7 +551,7 @@ __device__ __forceinline__ bool bvh_run(const KParams& P, const Ray& r, BvhQuery
                     while (cand != 0u) {
                         const uint32_t o = (first + (uint32_t)__builtin_ctz(cand)) * 16u;
                         cand &= cand - 1u;
-                        const float t = exact_t_geo<true>(leaf_geo(o), r, a4, a2);
+                        const float t = HRT_CAND_T ? candidate_t(leaf_geo(o), r, a4, a2) : exact_t_geo<true>(leaf_geo(o), r, a4, a2);
                         if (t > 0.0f && t <= bt) {  // beats(): a tie needs both slots (rare)
                             const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
                                 (void*)P.bvh_slot, (short)0, (int)(P.bvh_nleaf * 4u), 0x00020000);
@@ -753,13 +786,32 @@ __device__ __forceinline__ float div_by_radius(float x, float radius, float inv_
     return x / radius;
 }
 
+// div_by_radius of the three components with the guards as one wave-uniform branch (as sqrt_exact_u): the same bits
+__device__ __forceinline__ f3 div_by_radius3_u(f3 n, float radius, float inv_radius) {
+    const RcpRN d{radius, inv_radius};
+    f3 q = mk(div_rn_mid(n.x, d), div_rn_mid(n.y, d), div_rn_mid(n.z, d));
+    const float lo = fmin_ieee(fmin_ieee(__builtin_fabsf(n.x), __builtin_fabsf(n.y)), __builtin_fabsf(n.z));
+    const float hi = fmax_ieee(fmax_ieee(__builtin_fabsf(n.x), __builtin_fabsf(n.y)), __builtin_fabsf(n.z));
+    const bool slow = !(inv_radius != 0.0f && lo >= 0x1p-60f && hi <= 0x1p60f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) q = mk(div_by_radius(n.x, radius, inv_radius), div_by_radius(n.y, radius, inv_radius),
+                         div_by_radius(n.z, radius, inv_radius));
+    }
+    return q;
+}
+
 // The hit record from the hit point p = point_on_ray(o, d, t) (k_trace_split's packet-resolved primary rays carry p
-// instead of the origin; h.t is not read after the record is made)
+// instead of the origin; h.t is not read after the record is made). U: the guards as wave-uniform branches.
+template <bool U = false>
 __device__ __forceinline__ void sphere_record_p(const KParams& P, const f3 p, const f3 d, int bi, float t, Hit& h) {
     const SphereAux s = P.sph_aux[bi];
     f3 n = p - mk(s.cx, s.cy, s.cz);
-    n = mk(div_by_radius(n.x, s.radius, s.inv_radius), div_by_radius(n.y, s.radius, s.inv_radius),
-           div_by_radius(n.z, s.radius, s.inv_radius));
+    if constexpr (U) {
+        n = div_by_radius3_u(n, s.radius, s.inv_radius);
+    } else {
+        n = mk(div_by_radius(n.x, s.radius, s.inv_radius), div_by_radius(n.y, s.radius, s.inv_radius),
+               div_by_radius(n.z, s.radius, s.inv_radius));
+    }
     const bool front = dot(d, n) < 0.0f;
     if (!front) n = -n;
     h.p = p;
@@ -1309,14 +1361,14 @@ __device__ __forceinline__ f3 random_on_hemisphere(uint32_t& s, const f3& n) {
 // The three material arms share code so a wave holding several materials runs one hemisphere sample and
 // one final normalize instead of one per arm; every lane still performs exactly its own arm's operations
 // (and RNG draws) in the reference's order, so results are unchanged.
-template <int MODE>
+template <int MODE, bool U = false>  // U (sphere program): the exact sequences' guards as wave-uniform branches
 __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, const Hit& h) {
     const bool lambert = (h.id & 3u) == 1u, metal = (h.id & 3u) == 2u;
     f3 hemi = mk(0.0f, 0.0f, 0.0f);
     if (lambert || metal) hemi = random_on_hemisphere<MODE>(s, h.n);  // 3 draws, both arms
     f3 u = hemi;
     if (metal) {
-        const f3 in = MODE == MODE_SPHERE ? normalize_exact(r.d) : r.d;
+        const f3 in = MODE == MODE_SPHERE ? (U ? normalize_exact_u(r.d) : normalize_exact(r.d)) : r.d;
         u = reflect(in, h.n) + h.param * hemi;
     } else if (!lambert) {  // MAT_DIELECTRIC and the default arm
         // ir = front ? 1 / param : param, and reflectance's r0 * r0 for that ir, from the host (DielConsts)
@@ -1324,17 +1376,18 @@ __device__ __forceinline__ void scatter(const KParams& P, uint32_t& s, Ray& r, c
                                                                                      : &P.mats[h.id >> 3].inv_param;
         const float ir = h.front ? dc[0] : h.param;
         const float cos_t = fmin_ieee(dot(-r.d, h.n), 1.0f);
-        const float sin_t = MODE == MODE_SPHERE ? sqrt_exact(1.0f - cos_t * cos_t) : __builtin_sqrtf(1.0f - cos_t * cos_t);
+        const float sin_t = MODE == MODE_SPHERE ? (U ? sqrt_exact_u(1.0f - cos_t * cos_t) : sqrt_exact(1.0f - cos_t * cos_t))
+                                                : __builtin_sqrtf(1.0f - cos_t * cos_t);
         bool refl = ir * sin_t > 1.0f;  // cannot_refract; WGSL || short-circuits the RNG draw
         if (!refl) {
             const float f = rng_float(s);
             refl = reflectance_r0sq(cos_t, h.front ? dc[1] : dc[2]) > (f - __builtin_floorf(f));
         }
-        u = refl ? reflect(r.d, h.n) : refract<MODE == MODE_SPHERE>(r.d, h.n, ir);
+        u = refl ? reflect(r.d, h.n) : refract<MODE == MODE_SPHERE, U>(r.d, h.n, ir);
     }
     r.o = h.p;
     // (the triangle / mixed kernels keep the IEEE form: the fast one costs them spills)
-    r.d = lambert ? hemi : (MODE == MODE_SPHERE ? normalize_exact(u) : normalize(u));
+    r.d = lambert ? hemi : (MODE == MODE_SPHERE ? (U ? normalize_exact_u(u) : normalize_exact(u)) : normalize(u));
 }
 
 // (a, b) / sqrt(fma(b, b, a * a)) for two rng floats (each 0 or in [2^-32, 1]; the AA jitter and the disk direction
@@ -3014,8 +3067,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PACKET ? (S
                 if constexpr (!PACKET) queries++;
                 if (bi >= 0) {
                     Hit h;
-                    sphere_record_p(P, p, ray.d, bi, best, h);
-                    scatter<MODE>(P, s, ray, h);
+#ifndef HRT_UGUARD
+#define HRT_UGUARD 1
+#endif
+                    sphere_record_p<HRT_UGUARD != 0>(P, p, ray.d, bi, best, h);
+                    scatter<MODE, HRT_UGUARD != 0>(P, s, ray, h);
                     att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                     bounce++;
                     done = bounce >= P.bounces;
