@@ -821,8 +821,9 @@ __device__ __forceinline__ void sphere_record_p(const KParams& P, const f3 p, co
     h.id = ((uint32_t)bi << 3) | 4u | (s.id == 1u || s.id == 2u ? s.id : 0u);
     h.front = front;
 }
+template <bool U = false>
 __device__ __forceinline__ void sphere_record(const KParams& P, const Ray& r, int bi, float t, Hit& h) {
-    sphere_record_p(P, point_on_ray(r.o, r.d, t), r.d, bi, t, h);
+    sphere_record_p<U>(P, point_on_ray(r.o, r.d, t), r.d, bi, t, h);
 }
 
 // Coherent primary rays walked as one packet (k_trace_split<.., PACKET>). The 64 primary rays of
@@ -1305,7 +1306,7 @@ __device__ __forceinline__ void walk_sah(const KParams& /*P*/, const Ray& r, flo
     }
 }
 
-template <int MODE, int SCAN, bool TSAH = false>
+template <int MODE, int SCAN, bool TSAH = false, bool U = false>  // U: sphere_record_p<U>
 __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit& h, void* lds, Tally& tally,
                                             uint32_t* tri_cand, uint32_t* tri_stack) {
     float best = FLT_MAX_REF;
@@ -1333,7 +1334,7 @@ __device__ __forceinline__ bool closest_hit(const KParams& P, const Ray& r, Hit&
         return true;
     }
     if (bi >= 0) {
-        sphere_record(P, r, bi, best, h);
+        sphere_record<U>(P, r, bi, best, h);
         return true;
     }
     h.t = FLT_MAX_REF;
@@ -2480,6 +2481,9 @@ struct BlockState {
     uint32_t nblocks = 0;  // (diagnostic build: frame blocks this wave generated, for its wave record)
 #endif
 };
+#ifndef HRT_UGUARD_KTRACE
+#define HRT_UGUARD_KTRACE 1  // (k_trace's sphere program: the exact sequences' guards as wave-uniform branches)
+#endif
 template <int MODE, int SCAN, bool TSAH = false>
 // 6 waves per SIMD: the register budget is 80 VGPRs (84 unconstrained = 5 waves; measured +8% on C3)
 // (the mixed program's deferred scan holds 32 KB of LDS per workgroup: 5 waves/SIMD whatever the VGPRs)
@@ -2583,7 +2587,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #ifdef HRT_STAMPS
             const uint32_t boxes0 = tally.boxes;
 #endif
-            const bool hit = closest_hit<MODE, SCAN, TSAH>(P, ray, h, lds_list, tally, tri_cand, tri_stack);
+            constexpr bool UG = MODE == MODE_SPHERE && HRT_UGUARD_KTRACE != 0;
+            const bool hit = closest_hit<MODE, SCAN, TSAH, UG>(P, ray, h, lds_list, tally, tri_cand, tri_stack);
             queries++;
 #ifdef HRT_STAMPS
             st_ta = hrt_stamp();
@@ -2596,7 +2601,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             st_tb = st_ta;
 #endif
             if (hit) {
-                scatter<MODE>(P, s, ray, h);
+                scatter<MODE, UG>(P, s, ray, h);
                 att = att * mk(h.ar * 0.7f, h.ag * 0.7f, h.ab * 0.7f);
                 bounce++;
                 done = bounce >= P.bounces;
