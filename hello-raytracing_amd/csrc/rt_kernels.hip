@@ -1112,7 +1112,10 @@ __device__ __forceinline__ void heap_begin(const Ray& r, float best, HeapWalk& W
         const float lo = fmin_ieee(fmin_ieee(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)), __builtin_fabsf(r.d.z));
         const float hi = fmax_ieee(fmax_ieee(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)), __builtin_fabsf(r.d.z));
         W.inv = mk(rcp_rn_mid(r.d.x), rcp_rn_mid(r.d.y), rcp_rn_mid(r.d.z));
-        if (__builtin_expect(!(lo >= 0x1p-60f && hi <= 0x1p60f), 0)) W.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        const bool slow = !(lo >= 0x1p-60f && hi <= 0x1p60f);
+        if (__builtin_expect(__ballot(slow) != 0ull, 0)) {  // (a wave-uniform branch, as sqrt_exact_u)
+            if (slow) W.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        }
     } else {
         W.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     }
@@ -3146,6 +3149,12 @@ constexpr uint32_t heap_wg(int hl) { return hl == 3 ? 768u : 256u; }
 constexpr uint32_t heap_list_words(int hl, int scan) { return hl == 0 ? TRI_BATCH : (hl == 3 && scan != SCAN_BVH) ? 7u : 8u; }
 constexpr uint32_t heap_top_n(int hl, int scan) { return hl == 0 ? 0u : hl == 1 ? 256u : 1024u; }
 
+#ifndef HRT_HEAP_FAST_BVH
+#define HRT_HEAP_FAST_BVH 0  // (1: the culling-BVH mixed kernel (C5) takes heap_begin's refined reciprocals too: -0.2 %)
+#endif
+#ifndef HRT_UGUARD_TRIS
+#define HRT_UGUARD_TRIS 1  // (the mixed kernels' sphere hit record with the linear scan (C4): its normal division's guard as
+#endif                     //  a wave-uniform branch, +0.3 %; with the culling BVH (C5) -0.1 %, so not there)
 template <int MODE, int SCAN, int HL, bool STEAL>
 __global__ __launch_bounds__(heap_wg(HL)) __attribute__((amdgpu_waves_per_eu(SCAN == SCAN_DEFER ? 5 : 6))) void
 k_trace_split_tris(const KParams P) {
@@ -3229,7 +3238,7 @@ k_trace_split_tris(const KParams P) {
                 else if constexpr (SCAN == SCAN_DEFER) bi = scan_spheres_deferred(P, ray, sb, defer_list);
                 else bi = scan_spheres(P, ray, sb);
                 if constexpr (SCAN != SCAN_BVH) tally.spheres += P.nslots;  // the BVH scan counts its own
-                heap_begin<SCAN != SCAN_BVH>(ray, sb, W);
+                heap_begin<SCAN != SCAN_BVH || HRT_HEAP_FAST_BVH != 0>(ray, sb, W);
                 W.bj = -2 - bi;
                 qs = 3u;
             }
@@ -3266,7 +3275,7 @@ k_trace_split_tris(const KParams P) {
                 Hit h;
                 bool hit = true;
                 if (W.bj >= 0) tri_record(P, ray, P.tris[W.bj], W.best, h);
-                else if (W.bj <= -2) sphere_record(P, ray, -2 - W.bj, W.best, h);
+                else if (W.bj <= -2) sphere_record<HRT_UGUARD_TRIS != 0 && SCAN != SCAN_BVH>(P, ray, -2 - W.bj, W.best, h);
                 else hit = false;
                 if (hit) {
                     scatter<MODE>(P, s, ray, h);
