@@ -1423,17 +1423,42 @@ __device__ __forceinline__ float div_cam(float x, float l, float inv) {
 // fs_main prologue + make_ray (shader_sphere.wgsl:253-258, :123-135; shader_tris.wgsl:136-148).
 // FASTRNG: the jitter / disk / px, py divisions by the fast exact sequences (the sphere program everywhere; the other
 // programs' split kernels, whose frame-block refill has the registers for them — k_render<2, 4, false> spilled)
-template <int MODE, bool FASTRNG = (MODE == MODE_SPHERE)>
+// div_by_len_rng<true> / div_cam<true> with their guards as one wave-uniform branch (as sqrt_exact_u): the same bits
+__device__ __forceinline__ void div_by_len_rng_u(float a, float b, float& qa, float& qb) {
+    const float d = __builtin_fmaf(b, b, a * a);
+    const RcpRN r = rcp_rn_setup(sqrt_rn_mid(d));
+    qa = div_rn_mid(a, r);
+    qb = div_rn_mid(b, r);
+    const bool slow = !(d >= 0x1p-100f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) div_by_len_rng<false>(a, b, qa, qb);
+    }
+}
+__device__ __forceinline__ float div_cam_u(float x, float l, float inv) {
+    float q = div_rn_mid(x, RcpRN{l, inv});
+    const bool slow = !(inv != 0.0f && x >= 0x1p-60f && x <= 0x1p60f);
+    if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+        if (slow) q = x / l;
+    }
+    return q;
+}
+
+// U (sphere program, FASTRNG): the guards of the fast sequences as wave-uniform branches (k_trace's frame block, C2:
+// +0.9 %, profiles/r06/leaf_defer/ab_c2_uniform_guards_primary.txt; k_trace_split's measured -0.45 %,
+// ab_c3_uniform_guards_primary.txt)
+template <int MODE, bool FASTRNG = (MODE == MODE_SPHERE), bool U = false>
 __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uint32_t time, uint32_t& s) {
+    static_assert(!U || (FASTRNG && MODE == MODE_SPHERE), "uniform guards: the sphere program's fast sequences");
     s = (x * C->H + y) * time;
     const float r1 = rng_float(s);
     const float r2 = rng_float(s);
     float j1, j2;
-    div_by_len_rng<FASTRNG>(r1, r2, j1, j2);
+    if constexpr (U) div_by_len_rng_u(r1, r2, j1, j2);
+    else div_by_len_rng<FASTRNG>(r1, r2, j1, j2);
     const float px = ((float)x + 0.5f) + j1;
     const float py = ((float)y + 0.5f) + j2;
-    const float ux = (2.0f * div_cam<FASTRNG>(px, C->wm1, C->inv_wm1) - 1.0f) * C->aspect;
-    const float uy = (2.0f * div_cam<FASTRNG>(py, C->hm1, C->inv_hm1) - 1.0f) * -1.0f;
+    const float ux = (2.0f * (U ? div_cam_u(px, C->wm1, C->inv_wm1) : div_cam<FASTRNG>(px, C->wm1, C->inv_wm1)) - 1.0f) * C->aspect;
+    const float uy = (2.0f * (U ? div_cam_u(py, C->hm1, C->inv_hm1) : div_cam<FASTRNG>(py, C->hm1, C->inv_hm1)) - 1.0f) * -1.0f;
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) v[i] = ((C->right[i] * ux) * C->k + (C->up[i] * uy) * C->k) + C->dir[i];
@@ -1444,7 +1469,21 @@ __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uin
     const float vlo = fmin_ieee(fmin_ieee(__builtin_fabsf(v[0]), __builtin_fabsf(v[1])), __builtin_fabsf(v[2]));
     const float vhi = fmax_ieee(fmax_ieee(__builtin_fabsf(v[0]), __builtin_fabsf(v[1])),
                                 fmax_ieee(__builtin_fabsf(v[2]), __builtin_fabsf(v[3])));
-    if (MODE == MODE_SPHERE && vlo >= 0x1p-40f && vhi <= 0x1p40f) {
+    if constexpr (U) {
+        const float lv = sqrt_rn_mid(dv);
+        const RcpRN rl = rcp_rn_setup(lv);
+#pragma unroll
+        for (int i = 0; i < 3; i++) vn[i] = div_rn_mid(v[i], rl);
+        vn[3] = 0.0f;  // (unused by the sphere program: f4[3] is not read)
+        const bool slow = !(vlo >= 0x1p-40f && vhi <= 0x1p40f);
+        if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+            if (slow) {
+                const float l = __builtin_sqrtf(dv);
+#pragma unroll
+                for (int i = 0; i < 3; i++) vn[i] = v[i] / l;
+            }
+        }
+    } else if (MODE == MODE_SPHERE && vlo >= 0x1p-40f && vhi <= 0x1p40f) {
         const float lv = sqrt_rn_mid(dv);
         const RcpRN rl = rcp_rn_setup(lv);
 #pragma unroll
@@ -1462,7 +1501,8 @@ __device__ __forceinline__ Ray primary_ray(CamPtr C, uint32_t x, uint32_t y, uin
     const float q1 = rng_float(s);
     const float q2 = rng_float(s);
     float e1, e2;
-    div_by_len_rng<FASTRNG>(q1, q2, e1, e2);
+    if constexpr (U) div_by_len_rng_u(q1, q2, e1, e2);
+    else div_by_len_rng<FASTRNG>(q1, q2, e1, e2);
     const float rr = rng_float(s) * C->blur;
     float o4[4];
     o4[0] = C->eye[0] + e1 * rr;
@@ -2222,7 +2262,11 @@ __device__ __forceinline__ void refill_block(const KParams& P, BlockQueue& B, co
             B.pr_ok = (x < P.W && kr < P.nrows) ? 1u : 0u;  // ragged edge tiles: no sample
             if (B.pr_ok) {
                 const uint32_t y = global_row(P.row0, P.row_block, P.row_stride, kr);
-                const Ray pr = primary_ray<MODE>(&kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
+#ifndef HRT_UGUARD_KTRACE_PRIMARY
+#define HRT_UGUARD_KTRACE_PRIMARY 1
+#endif
+                const Ray pr = primary_ray<MODE, MODE == MODE_SPHERE, MODE == MODE_SPHERE && HRT_UGUARD_KTRACE_PRIMARY != 0>(
+                    &kargs()->cam, x, y, P.time0 + (B.job_f0 + B.blk_f) * P.dtime, B.pr_s);
                 B.pr_o = pr.o;
                 B.pr_d = pr.d;
             }
